@@ -1,0 +1,207 @@
+#!/usr/bin/env python
+"""Scheduling decisions/sec on BASELINE.json configs[1]: 1024 TPC-H-format envs per GPU, 50 jobs /
+10 executors, uniform-random valid actions from the device RNG (the reference's examples.py ENV_CFG).
+
+A "step" = one env.step for every env of the batch: device random policy reads the obs, then the step
+kernel applies the action, runs the discrete-event loop and writes the next observation to HBM.
+Modes: `rollout` (default: K steps of policy+step fused into one persistent launch) and `step`
+(two launches per step, the C-ABI call pattern of an external policy).
+
+Output: one JSON line on rank 0. Multi-GPU: one process per GPU (torchrun), envs sharded per rank with
+no data-path collective (weak scaling); decisions are summed and time is max-reduced over ranks.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "gym-sparksched_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+ENV_CFG = {"num_executors": 10, "job_arrival_cap": 50, "job_arrival_rate": 4.0e-5, "moving_delay": 2000.0,
+           "warmup_delay": 1000.0}  # examples.py:15-23
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def _cpu_worker(args):
+    """One reference-style rollout worker (trainers/rollout_worker.py:53-95): one env per process,
+    torch.set_num_threads(1)-equivalent single thread, RandomScheduler(seed), episodes back to back."""
+    seed, seconds = args
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "gym-sparksched_amd"))
+    from oracle.policies import RandomPolicy
+    from oracle.restatement import SparkSchedOracle
+    from spark_sched_sim.data_samplers.synthetic_tpch import generate
+
+    ds = generate(0)
+    env = SparkSchedOracle(ENV_CFG, ds)
+    pol = RandomPolicy(42 + seed)
+    env.reset(seed=seed)  # warm-up episode start (not counted)
+    decisions, t0, ep = 0, time.perf_counter(), 0
+    obs, _ = env.reset(seed=seed)
+    while time.perf_counter() - t0 < seconds:
+        a, _ = pol.schedule(obs)
+        obs, _, done, _, _ = env.step(a)
+        decisions += 1
+        if done:
+            ep += 1
+            obs, _ = env.reset(seed=seed + 1000 * ep)
+    return decisions, time.perf_counter() - t0
+
+
+def cpu_baseline(seconds: float, procs: int) -> dict:
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(7 + i, seconds) for i in range(procs)])
+    dec = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return {"value": dec / wall, "unit": "decisions/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} spawn processes x {seconds:.0f}s of config-2 episodes (J=50, N=10), one env per "
+                      "process, RandomScheduler(seed) — the CPU oracle restatement (real CPython set/dict/heapq, "
+                      "numpy Generator), mirroring trainers/rollout_worker.py"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
+    ap.add_argument("--mode", choices=["rollout", "step"], default="rollout")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from spark_sched_sim import _abi
+    from spark_sched_sim.data_samplers.synthetic_tpch import generate
+    from spark_sched_sim.engine import DeviceEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device(f"cuda:{local}")
+
+    B, K, W = args.envs, args.steps, args.warmup
+    eng = DeviceEngine(ENV_CFG, B, generate(0), device=dev)
+    eng.reset(seeds=[args.seed + rank * B + i for i in range(B)])
+    kind = _abi.SSIM_POLICY_RANDOM
+    stream = torch.cuda.current_stream(dev)
+
+    def run(n, events=None):
+        if args.mode == "rollout":
+            if events is not None:
+                events[0].record(stream)
+            eng.rollout(kind, 1234, n)
+            if events is not None:
+                events[1].record(stream)
+        else:
+            for k in range(n):
+                si, ne = eng.policy(kind, 1234, run.counter)
+                run.counter += 1
+                if events is not None:
+                    events[2 * k].record(stream)
+                eng.step(si, ne)
+                if events is not None:
+                    events[2 * k + 1].record(stream)
+    run.counter = 0
+
+    run(W)
+    torch.cuda.synchronize(dev)
+    counts0 = eng.views["counts"].cpu().numpy().copy()
+    acc0 = eng.views["acc"].cpu().numpy().copy()
+    n_ev = 2 if args.mode == "rollout" else 2 * K
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(K, events)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    counts1 = eng.views["counts"].cpu().numpy()
+    acc1 = eng.views["acc"].cpu().numpy()
+    errs = int(np.count_nonzero(counts1[:, _abi.OC_ERR] & _abi.SSIM_ERR_STICKY))
+    decisions = int((counts1[:, _abi.OC_DECISIONS] - counts0[:, _abi.OC_DECISIONS]).sum())
+    terminated = int(counts1[:, _abi.OC_TERMINATED].sum())
+    d_acc = (acc1 - acc0).sum(axis=0).astype(np.float64)  # S_act, E_act, J_act, events
+    # B_dec = 36 S_act + 20 E_act + 16 J_act + 96 K + 40 bytes per decision
+    alg_bytes = 36 * d_acc[0] + 20 * d_acc[1] + 16 * d_acc[2] + 96 * d_acc[3] + 40 * decisions
+    if args.mode == "rollout":
+        kern_ms = events[0].elapsed_time(events[1])
+        launches = 1
+    else:
+        kern_ms = sum(events[2 * k].elapsed_time(events[2 * k + 1]) for k in range(K))
+        launches = K
+    elapsed = t1 - t0
+    stats = torch.tensor([elapsed, float(decisions), alg_bytes, kern_ms, float(errs), float(terminated)],
+                         dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = stats[0:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        rest = stats[1:].clone()
+        dist.all_reduce(rest, op=dist.ReduceOp.SUM)
+        stats = torch.cat([tmax, rest])
+        # episode statistics gather (the only collective; RCCL all_gather, off the timed path)
+        mine = torch.tensor(counts1[:, [_abi.OC_NUM_COMPLETED, _abi.OC_NUM_ARRIVED, _abi.OC_DECISIONS]],
+                            dtype=torch.int32, device=dev)
+        gathered = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+    elapsed, decisions, alg_bytes, kern_ms_sum, errs, terminated = stats.tolist()
+    kern_ms = kern_ms_sum / world
+    value = decisions / elapsed
+    achieved = (alg_bytes / world / launches) / (kern_ms / launches / 1e3) / 1e9  # GB/s per GPU, dominant kernel
+    if rank == 0:
+        line = {
+            "metric": "scheduling decisions/sec (env steps/s)",
+            "value": value,
+            "unit": "decisions/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": elapsed * 1e3 / K,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64+i32",
+            "data": "synthetic TPC-H-format dataset (seeded generator), random valid actions (device RNG)",
+            "config": {"workload": f"{B} envs/GPU x TPC-H 50 jobs / 10 executors (BASELINE configs[1])",
+                       "envs_per_gpu": B, "jobs": 50, "executors": 10, "mode": args.mode,
+                       "parallelism": f"env-sharded x{world}"},
+            "decisions": int(decisions),
+            "terminated_envs": int(terminated),
+            "frozen_envs": int(errs),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_rollout" if args.mode == "rollout" else "k_step",
+                         "kernel_ms_per_launch": kern_ms / launches,
+                         "alg_bytes_per_launch": alg_bytes / world / launches},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, procs)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

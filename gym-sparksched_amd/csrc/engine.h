@@ -1,0 +1,1104 @@
+// engine.h — the batched Spark-scheduling simulation step, one wavefront per env.
+//
+// Restates the hot path of spark_sched_sim/spark_sched_sim.py (reset 127-186, step 188-221, the event
+// loop 320-343, handlers 428-483, helpers 487-874), components/executor_tracker.py and
+// data_samplers/tpch.py:75-106 on device-resident structure-of-arrays state (layout.h).
+//
+// Execution model. Control flow is wave-uniform: every lane of the env's wavefront executes the serial
+// part of the algorithm with identical values, so branches never diverge and same-address loads are
+// broadcast. Data-parallel parts run across lanes through the W policy: the schedulable-stage scan
+// (ballot + first-set-lane), executor event-slot argmin (min-reduce), observation rows and edges
+// (ballot/prefix compaction, coalesced stores), pool-table iteration. W is WaveHip on device
+// (sparksched.hip); the test-only host build (tests/hostsim/) instantiates the same template with a
+// one-lane W to debug the logic on CPU. Everything stays in the device's memory spaces: state in HBM
+// (env-major SoA), per-launch scratch in LDS.
+#pragma once
+#include <stdint.h>
+
+#include "layout.h"
+#include "pcg64.h"
+#include "pyset.h"
+
+namespace ssim {
+
+enum : int32_t { kPoolNone = -1, kPoolCommon = 0 };
+enum : int32_t { kEvArrival = 1, kEvTask = 2, kEvReady = 3, kTrJobDone = 4 };
+enum : int32_t { kJobPending = 0, kJobActive = 1, kJobDone = 2 };
+enum : int32_t { kScanAll = 0, kScanOnly = 1, kScanExcept = 2 };
+
+struct StepIn {
+  int32_t stage_idx, num_exec;
+};
+
+// Everything a launch needs besides the arenas. Lives at the start of the state arena (device memory),
+// so kernels take one pointer and read fields through the scalar cache.
+struct Params {
+  ssim_layout L;
+  StateOffsets O;
+  ssim_dataset D;
+  ssim_config C;
+};
+constexpr int64_t kParamsReserve = 4096;
+static_assert(sizeof(Params) <= kParamsReserve, "params block");
+
+template <class W>
+struct Sim {
+  const ssim_layout& L;
+  const StateOffsets& O;
+  const ssim_dataset& D;
+  const ssim_config& C;
+  uint8_t* env;  // this env's state block
+  uint8_t* scr;  // this env's scratch block
+  uint8_t* obs;  // obs arena base
+  int32_t eid;   // env index
+  EnvHeader h;   // register copy of the header
+  Pcg64 rng;
+
+  __device__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* scratch, uint8_t* obs_arena,
+                 int32_t env_index)
+      : L(p->L), O(p->O), D(p->D), C(p->C),
+        env(state_arena + kParamsReserve + (int64_t)env_index * p->L.env_bytes), scr(scratch),
+        obs(obs_arena), eid(env_index) {}
+
+  // ---------------------------------------------------------------- field access
+  template <class T>
+  __device__ __forceinline__ T* F(int64_t off) const {
+    return reinterpret_cast<T*>(env + off);
+  }
+  template <class T>
+  __device__ __forceinline__ T* S(int64_t off) const {
+    return reinterpret_cast<T*>(scr + off);
+  }
+  __device__ __forceinline__ void load_header() {
+    h = *F<EnvHeader>(O.hdr);
+    rng.s_hi = h.rng_s_hi;
+    rng.s_lo = h.rng_s_lo;
+    rng.i_hi = h.rng_i_hi;
+    rng.i_lo = h.rng_i_lo;
+    rng.has32 = h.rng_has32;
+    rng.u32 = h.rng_u32;
+  }
+  __device__ __forceinline__ void store_header() {
+    h.rng_s_hi = rng.s_hi;
+    h.rng_s_lo = rng.s_lo;
+    h.rng_i_hi = rng.i_hi;
+    h.rng_i_lo = rng.i_lo;
+    h.rng_has32 = rng.has32;
+    h.rng_u32 = rng.u32;
+    W::sync();
+    if (W::lane() == 0) *F<EnvHeader>(O.hdr) = h;
+    W::sync();
+  }
+  __device__ __forceinline__ void fail(uint32_t bits) { h.err |= bits; }
+  __device__ __forceinline__ bool frozen() const { return (h.err & SSIM_ERR_STICKY) != 0u; }
+  __device__ __forceinline__ void check(bool ok) {
+    if (!ok) h.err |= SSIM_ERR_INVARIANT;
+  }
+
+  // stages (env-global index g = job_base[j] + local stage id)
+  __device__ __forceinline__ int32_t& st_job(int g) const { return F<int32_t>(O.st_job)[g]; }
+  __device__ __forceinline__ int32_t& st_ts(int g) const { return F<int32_t>(O.st_ts)[g]; }
+  __device__ __forceinline__ int32_t& st_rem(int g) const { return F<int32_t>(O.st_rem)[g]; }
+  __device__ __forceinline__ int32_t& st_exe(int g) const { return F<int32_t>(O.st_exe)[g]; }
+  __device__ __forceinline__ int32_t& st_done(int g) const { return F<int32_t>(O.st_done)[g]; }
+  __device__ __forceinline__ int32_t& st_mov(int g) const { return F<int32_t>(O.st_mov)[g]; }
+  __device__ __forceinline__ int32_t& st_com(int g) const { return F<int32_t>(O.st_com)[g]; }
+  __device__ __forceinline__ int32_t& st_unmet(int g) const { return F<int32_t>(O.st_unmet)[g]; }
+  __device__ __forceinline__ int32_t& st_sel(int g) const { return F<int32_t>(O.st_sel)[g]; }
+  __device__ __forceinline__ double& st_recent(int g) const { return F<double>(O.st_recent)[g]; }
+  __device__ __forceinline__ int32_t ntasks(int g) const { return D.ts_num_tasks[st_ts(g)]; }
+  __device__ __forceinline__ bool st_completed(int g) const { return st_done(g) == ntasks(g); }
+  // jobs
+  __device__ __forceinline__ int32_t& job_tpl(int j) const { return F<int32_t>(O.job_tpl)[j]; }
+  __device__ __forceinline__ int32_t& job_base(int j) const { return F<int32_t>(O.job_base)[j]; }
+  __device__ __forceinline__ int32_t& job_nst(int j) const { return F<int32_t>(O.job_nst)[j]; }
+  __device__ __forceinline__ int32_t& job_nact(int j) const { return F<int32_t>(O.job_nact)[j]; }
+  __device__ __forceinline__ int32_t& job_sat(int j) const { return F<int32_t>(O.job_sat)[j]; }
+  __device__ __forceinline__ int32_t& job_local(int j) const { return F<int32_t>(O.job_local)[j]; }
+  __device__ __forceinline__ int32_t& job_supply(int j) const { return F<int32_t>(O.job_supply)[j]; }
+  __device__ __forceinline__ int32_t& job_state(int j) const { return F<int32_t>(O.job_state)[j]; }
+  __device__ __forceinline__ int32_t& job_arr_dec(int j) const { return F<int32_t>(O.job_arr_dec)[j]; }
+  __device__ __forceinline__ int32_t& job_done_dec(int j) const { return F<int32_t>(O.job_done_dec)[j]; }
+  __device__ __forceinline__ double& job_tarr(int j) const { return F<double>(O.job_tarr)[j]; }
+  __device__ __forceinline__ double& job_tdone(int j) const { return F<double>(O.job_tdone)[j]; }
+  // executors
+  __device__ __forceinline__ int32_t& ex_loc(int e) const { return F<int32_t>(O.ex_loc)[e]; }
+  __device__ __forceinline__ int32_t& ex_job(int e) const { return F<int32_t>(O.ex_job)[e]; }
+  __device__ __forceinline__ int32_t& ex_task(int e) const { return F<int32_t>(O.ex_task)[e]; }
+  __device__ __forceinline__ int32_t& ex_busy(int e) const { return F<int32_t>(O.ex_busy)[e]; }
+  __device__ __forceinline__ double& ev_t(int e) const { return F<double>(O.ev_t)[e]; }
+  __device__ __forceinline__ int32_t& ev_seq(int e) const { return F<int32_t>(O.ev_seq)[e]; }
+  __device__ __forceinline__ int32_t& ev_type(int e) const { return F<int32_t>(O.ev_type)[e]; }
+  __device__ __forceinline__ int32_t& ev_stage(int e) const { return F<int32_t>(O.ev_stage)[e]; }
+  // pools: code 0 = COMMON, 1+j = job j, 1+job_cap+g = stage g, -1 = None
+  __device__ __forceinline__ int32_t job_pool(int j) const { return 1 + j; }
+  __device__ __forceinline__ int32_t stage_pool(int g) const { return 1 + L.job_cap + g; }
+  __device__ __forceinline__ bool is_stage_pool(int p) const { return p > L.job_cap; }
+  __device__ __forceinline__ int32_t pool_stage(int p) const { return p - 1 - L.job_cap; }
+  __device__ __forceinline__ int32_t pool_job(int p) const {  // pool_key[0]; -1 = None
+    if (p <= 0) return -1;
+    if (p <= L.job_cap) return p - 1;
+    return st_job(p - 1 - L.job_cap);
+  }
+  __device__ __forceinline__ PySetMeta* pmeta(int p) const { return F<PySetMeta>(O.pool_meta) + p; }
+  __device__ __forceinline__ uint8_t* ptab(int p) const { return F<uint8_t>(O.pool_tab) + (int64_t)p * L.set_cap; }
+  __device__ __forceinline__ int32_t& cfrom(int p) const { return F<int32_t>(O.pool_cfrom)[p]; }
+  __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)pmeta(p)->used; }
+
+  // ---------------------------------------------------------------- tracker (executor_tracker.py)
+  __device__ int32_t source_job() const {  // :98-102
+    return (h.source <= kPoolCommon) ? -1 : pool_job(h.source);
+  }
+  __device__ int committable() {  // :105-111 (pool None is always empty with no commitments)
+    if (h.source < 0) return 0;
+    const int n = pool_size(h.source) - cfrom(h.source);
+    check(n >= 0);
+    return n;
+  }
+  __device__ int demand(int g) const { return st_rem(g) - (st_mov(g) + st_com(g)); }  // :566-578
+
+  __device__ void supply_add(int job, int n) {
+    if (job < 0)
+      h.supply_none += n;
+    else
+      job_supply(job) += n;
+  }
+
+  __device__ void add_commitment(int n, int dst) {  // :146-154, 224-236
+    const int src = h.source;
+    check(src >= 0);
+    if (src < 0) return;
+    int32_t* cs = F<int32_t>(O.cm_src);
+    int32_t* cd = F<int32_t>(O.cm_dst);
+    int32_t* cc = F<int32_t>(O.cm_cnt);
+    int32_t* co = F<int32_t>(O.cm_ord);
+    int hit = -1, freeslot = -1;
+    for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      const bool ok = k < L.commit_cap;
+      const int cnt = ok ? cc[k] : 0;
+      const uint64_t mh = W::ballot(ok && cnt > 0 && cs[k] == src && cd[k] == dst);
+      const uint64_t mf = W::ballot(ok && cnt == 0);
+      if (hit < 0 && mh) hit = k0 + W::ffs(mh);
+      if (freeslot < 0 && mf) freeslot = k0 + W::ffs(mf);
+    }
+    W::sync();
+    if (hit >= 0) {
+      if (W::lane() == 0) cc[hit] += n;
+    } else if (freeslot >= 0) {
+      if (W::lane() == 0) {
+        cs[freeslot] = src;
+        cd[freeslot] = dst;
+        cc[freeslot] = n;
+        co[freeslot] = h.commit_seq;
+      }
+      h.commit_seq++;
+    } else {
+      fail(SSIM_ERR_CAPACITY);
+      return;
+    }
+    W::sync();
+    cfrom(src) += n;
+    if (is_stage_pool(dst)) st_com(pool_stage(dst)) += n;
+    check(pool_size(src) >= cfrom(src));
+    const int sj = pool_job(src), dj = pool_job(dst);
+    if (dj != sj) supply_add(dj, n);
+  }
+
+  __device__ int find_commit(int src, int dst) {
+    const int32_t* cs = F<int32_t>(O.cm_src);
+    const int32_t* cd = F<int32_t>(O.cm_dst);
+    const int32_t* cc = F<int32_t>(O.cm_cnt);
+    for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      const uint64_t m = W::ballot(k < L.commit_cap && cc[k] > 0 && cs[k] == src && cd[k] == dst);
+      if (m) return k0 + W::ffs(m);
+    }
+    return -1;
+  }
+
+  __device__ int remove_commitment(int e, int dst) {  // :156-173, 238-249; returns src
+    const int src = ex_loc(e);
+    check(src >= 0);
+    const int k = src >= 0 ? find_commit(src, dst) : -1;
+    if (k < 0) {
+      fail(SSIM_ERR_INVARIANT);  // ValueError("no commitments from ...") in the reference
+      return src;
+    }
+    W::sync();
+    int32_t* cc = F<int32_t>(O.cm_cnt);
+    const int left = cc[k] - 1;
+    W::sync();
+    if (W::lane() == 0) cc[k] = left;
+    W::sync();
+    cfrom(src) -= 1;
+    check(cfrom(src) >= 0);
+    if (is_stage_pool(dst)) {
+      st_com(pool_stage(dst)) -= 1;
+      check(st_com(pool_stage(dst)) >= 0);
+    }
+    const int sj = pool_job(src), dj = pool_job(dst);
+    if (dj != sj) {
+      supply_add(dj, -1);
+      check(dj < 0 ? h.supply_none >= 0 : job_supply(dj) >= 0);
+    }
+    return src;
+  }
+
+  __device__ int peek_commitment(int p) {  // :175-180: first key in insertion order, -1 = None
+    const int32_t* cs = F<int32_t>(O.cm_src);
+    const int32_t* cd = F<int32_t>(O.cm_dst);
+    const int32_t* cc = F<int32_t>(O.cm_cnt);
+    const int32_t* co = F<int32_t>(O.cm_ord);
+    int best_ord = 0x7FFFFFFF, best_dst = kPoolNone;
+    for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      const bool ok = k < L.commit_cap && cc[k] > 0 && cs[k] == p;
+      int ord = ok ? co[k] : 0x7FFFFFFF;
+      int dst = ok ? cd[k] : kPoolNone;
+      W::min_pair(ord, dst);
+      if (ord < best_ord) {
+        best_ord = ord;
+        best_dst = dst;
+      }
+    }
+    return best_dst;
+  }
+
+  // Snapshot of commitments[src] in insertion order into scratch plan: (dst, count) pairs.
+  __device__ int commit_plan(int src, int32_t* plan) {
+    const int32_t* cs = F<int32_t>(O.cm_src);
+    const int32_t* cd = F<int32_t>(O.cm_dst);
+    const int32_t* cc = F<int32_t>(O.cm_cnt);
+    const int32_t* co = F<int32_t>(O.cm_ord);
+    int n = 0, last = -1;
+    for (;;) {  // selection by increasing insertion stamp (live entries <= N)
+      int ord = 0x7FFFFFFF, k_best = -1;
+      for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+        const int k = k0 + W::lane();
+        const bool ok = k < L.commit_cap && cc[k] > 0 && cs[k] == src && co[k] > last;
+        int o = ok ? co[k] : 0x7FFFFFFF;
+        int kk = ok ? k : -1;
+        W::min_pair(o, kk);
+        if (o < ord) {
+          ord = o;
+          k_best = kk;
+        }
+      }
+      if (k_best < 0) break;
+      const int dst = cd[k_best], cnt = cc[k_best];
+      W::sync();
+      if (W::lane() == 0) {
+        plan[2 * n] = dst;
+        plan[2 * n + 1] = cnt;
+      }
+      W::sync();
+      n++;
+      last = ord;
+    }
+    return n;
+  }
+
+  __device__ void pool_add(int p, int e) {
+    int32_t* tmp = S<int32_t>(O.sc_keys_b);
+    if (W::lane() == 0) ps_add(pmeta(p), ptab(p), (uint32_t)e, tmp);
+    W::sync();
+  }
+  __device__ void pool_remove(int p, int e) {
+    int ok = 1;
+    if (W::lane() == 0) ok = ps_remove(pmeta(p), ptab(p), (uint32_t)e) ? 1 : 0;
+    ok = W::bcast_i(ok, 0);
+    W::sync();
+    check(ok != 0);
+  }
+
+  __device__ void move_to_pool(int e, int dst, bool send) {  // :186-220
+    const int old = ex_loc(e);
+    if (old >= 0) {
+      pool_remove(old, e);
+      ex_loc(e) = kPoolNone;
+    }
+    if (!send) {
+      ex_loc(e) = dst;
+      pool_add(dst, e);
+      return;
+    }
+    const int g = pool_stage(dst);
+    st_mov(g) += 1;
+    const int oj = old >= 0 ? pool_job(old) : -1;
+    const int nj = st_job(g);
+    check(oj != nj);
+    job_supply(nj) += 1;
+    if (oj >= 0) {
+      job_supply(oj) -= 1;
+      check(job_supply(oj) >= 0);
+    }
+  }
+
+  // Table order of set(e for e in pool.copy() if not busy) — _get_idle_source_executors (:714-728).
+  __device__ int idle_order(int p, int32_t* out) {
+    if (p < 0) return 0;
+    int n = 0;
+    if (W::lane() == 0) {
+      const PySetMeta* m = pmeta(p);
+      n = ps_keys(m, ptab(p), out);
+      ps_copy_order(m, out, n, S<uint8_t>(O.sc_tab_a));
+      int k = 0;
+      for (int i = 0; i < n; ++i)
+        if (!ex_busy(out[i])) out[k++] = out[i];
+      n = k;
+      ps_build_order(out, n, S<uint8_t>(O.sc_tab_b), S<int32_t>(O.sc_keys_b));
+    }
+    n = W::bcast_i(n, 0);
+    W::sync();
+    return n;
+  }
+
+  // ---------------------------------------------------------------- events (event.py)
+  __device__ void push_event(int e, double t, int type, int g) {
+    check(ev_seq(e) < 0);  // at most one pending event per executor (DESIGN.md §Event queue)
+    ev_t(e) = t;
+    ev_seq(e) = h.seq++;
+    ev_type(e) = type;
+    ev_stage(e) = g;
+  }
+
+  __device__ void trace(double t, int kind, int e, int job, int sid, int seq) {
+    if (h.trace_len < L.trace_cap && W::lane() == 0) {
+      TraceRec* r = reinterpret_cast<TraceRec*>(obs + L.ob_trace) + (int64_t)eid * L.trace_cap + h.trace_len;
+      r->t = t;
+      r->kind = kind;
+      r->exec = e;
+      r->job = job;
+      r->stage = sid;
+      r->seq = seq;
+      r->pad = 0;
+    }
+    h.trace_len++;
+  }
+
+  // ---------------------------------------------------------------- sampler (tpch.py:75-106, 208-235)
+  __device__ bool draw(int ts, int wave, int level, double* out) {
+    const int idx = (ts * 3 + wave) * kNumLevels + level;
+    const int len = D.dur_len[idx];
+    if (len <= 0) return false;  // KeyError (missing) or ValueError (empty): no RNG consumed
+    const uint32_t k = rng.bounded((uint32_t)len);
+    *out = D.durations[D.dur_off[idx] + (int)k];
+    return true;
+  }
+
+  __device__ double task_duration(int j, int g, int e) {
+    const int n_local = job_local(j);
+    check(n_local > 0);
+    const int ts = st_ts(g);
+    const double lo = D.intervals[2 * n_local], hi = D.intervals[2 * n_local + 1];
+    double key;
+    if (lo == hi) {
+      key = lo;
+    } else {
+      const int pt = 1 + (int)(rng.random() * (hi - lo));
+      key = ((double)pt <= (double)n_local - lo) ? lo : hi;
+    }
+    int level = -1;
+    const double levels[kNumLevels] = {5, 10, 20, 40, 50, 60, 80, 100};
+    for (int l = 0; l < kNumLevels; ++l)
+      if (key == levels[l]) level = l;
+    if (level < 0 || !((D.ts_fw_keymask[ts] >> level) & 1)) level = D.ts_fw_maxlevel[ts];
+    double d = 0.0;
+    const int last = ex_task(e);
+    if (last < 0) {
+      if (draw(ts, 0, level, &d)) return d;
+      if (draw(ts, 1, level, &d)) return d + C.warmup_delay;
+      fail(SSIM_ERR_SAMPLER);
+      return 0.0;
+    }
+    if (last == g - job_base(j)) {
+      if (draw(ts, 2, level, &d)) return d;
+    }
+    if (draw(ts, 1, level, &d)) return d;
+    if (draw(ts, 0, level, &d)) return d;
+    fail(SSIM_ERR_SAMPLER);
+    return 0.0;
+  }
+
+  // ---------------------------------------------------------------- schedulable-stage search (:505-555)
+  __device__ bool stage_pred(int g, int mode, int jx, int src_job) const {
+    const int j = st_job(g);
+    if (mode == kScanOnly && j != jx) return false;
+    if (mode == kScanExcept && j == jx) return false;
+    if (!(j == src_job || job_supply(j) < L.num_executors)) return false;
+    if (st_sel(g)) return false;
+    if (demand(g) <= 0) return false;
+    const int ts = st_ts(g), base = job_base(j);
+    for (int k = D.ts_parent_base[ts]; k < D.ts_parent_base[ts + 1]; ++k)
+      if (demand(base + D.ts_parents[k]) > 0) return false;
+    return true;
+  }
+
+  // first schedulable stage in node order, or -1
+  __device__ int scan_first(int mode, int jx, int src_job) {
+    const int n = h.n_active_stages;
+    const int32_t* act = F<int32_t>(O.active_stages);
+    for (int i0 = 0; i0 < n; i0 += W::kWidth) {
+      const int i = i0 + W::lane();
+      const int g = i < n ? act[i] : -1;
+      const uint64_t m = W::ballot(g >= 0 && stage_pred(g, mode, jx, src_job));
+      if (m) return W::bcast_i(g, W::ffs(m));
+    }
+    return -1;
+  }
+  __device__ bool any_schedulable() { return scan_first(kScanAll, -1, source_job()) >= 0; }
+
+  __device__ int find_backup(int e) {  // :821-845 (quirks Q1/Q2)
+    const int jx = ex_job(e);
+    check(jx >= 0);
+    const int sj = (jx == 0 || jx < 0) ? source_job() : jx;  // `if not source_job_id`
+    int g = scan_first(kScanOnly, jx, sj);
+    if (g >= 0) return g;
+    const bool others = h.n_active_jobs > ((jx >= 0 && job_state(jx) == kJobActive) ? 1 : 0);
+    return scan_first(others ? kScanExcept : kScanAll, jx, sj);  // `if not job_ids`: [] -> all
+  }
+
+  // ---------------------------------------------------------------- list maintenance
+  __device__ void list_remove(int32_t* list, int n, int value) {  // ordered removal by wave shift
+    int pos = -1;
+    for (int i0 = 0; i0 < n && pos < 0; i0 += W::kWidth) {
+      const int i = i0 + W::lane();
+      const uint64_t m = W::ballot(i < n && list[i] == value);
+      if (m) pos = i0 + W::ffs(m);
+    }
+    check(pos >= 0);
+    if (pos < 0) return;
+    for (int i0 = pos; i0 < n - 1; i0 += W::kWidth) {
+      const int i = i0 + W::lane();
+      const int v = (i < n - 1) ? list[i + 1] : 0;
+      W::sync();
+      if (i < n - 1) list[i] = v;
+      W::sync();
+    }
+  }
+
+  // ---------------------------------------------------------------- movement state machine
+  __device__ void detach(int j, int e) {  // job.py:84-89
+    check(ex_job(e) == j);
+    job_local(j) -= 1;
+    ex_job(e) = -1;
+    ex_task(e) = -1;
+  }
+
+  __device__ void run_next_task(int e, int g) {  // :584-615
+    const int j = st_job(g);
+    check(st_rem(g) > 0);
+    check(ex_job(e) == j);
+    check(!ex_busy(e));
+    st_rem(g) -= 1;
+    st_exe(g) += 1;
+    if (st_rem(g) == 0) job_sat(j) += 1;
+    const double dur = task_duration(j, g, e);
+    ex_task(e) = g - job_base(j);
+    ex_busy(e) = 1;
+    st_recent(g) = dur;
+    push_event(e, h.wall + dur, kEvTask, g);
+  }
+
+  __device__ void send(int e, int g) {  // :617-637
+    check(!ex_busy(e));
+    check(ex_job(e) != st_job(g));
+    move_to_pool(e, stage_pool(g), true);
+    if (ex_job(e) >= 0) detach(ex_job(e), e);
+    push_event(e, h.wall + C.moving_delay, kEvReady, g);
+  }
+
+  // _move_idle_executors (:745-782) with an explicit executor list (n ids in `ids`).
+  __device__ void release_idle_list(int src, const int32_t* ids, int n) {
+    if (src < 0) src = h.source;
+    check(src >= 0);
+    if (src <= kPoolCommon) return;
+    check(n > 0);
+    const int j = pool_job(src);
+    const bool sat = job_sat(j) == job_nst(j);
+    if (!is_stage_pool(src) && !sat) return;
+    const int dst = sat ? kPoolCommon : job_pool(j);
+    for (int k = 0; k < n; ++k) {
+      const int e = ids[k];
+      move_to_pool(e, dst, false);
+      if (dst == kPoolCommon) detach(j, e);
+    }
+  }
+  __device__ void release_idle_one(int src, int e) {
+    int32_t one = e;
+    release_idle_list(src, &one, 1);
+  }
+  __device__ void release_idle_all(int src) {
+    if (src < 0) src = h.source;
+    check(src >= 0);
+    if (src <= kPoolCommon) return;
+    int32_t* ids = S<int32_t>(O.sc_keys_a);
+    const int n = idle_order(src, ids);
+    release_idle_list(src, ids, n);
+  }
+
+  __device__ void goto_stage(int e, int g) {  // _move_executor_to_stage :799-819 (+ backup loop)
+    for (int guard = 0; guard < 4 * L.stage_cap + 8; ++guard) {
+      if (st_rem(g) == 0) {  // _try_backup_schedule :784-797
+        const int b = find_backup(e);
+        if (b >= 0) {
+          g = b;
+          continue;
+        }
+        release_idle_one(ex_loc(e), e);
+        return;
+      }
+      const int j = st_job(g);
+      if (ex_job(e) != j) {
+        send(e, g);
+        return;
+      }
+      if (st_unmet(g) != 0) {  // not in job.frontier_stages
+        ex_task(e) = -1;
+        move_to_pool(e, job_pool(j), false);
+        return;
+      }
+      move_to_pool(e, stage_pool(g), false);
+      run_next_task(e, g);
+      return;
+    }
+    fail(SSIM_ERR_INVARIANT);
+  }
+
+  __device__ void fulfill(int e, int dst) {  // :699-712
+    const int src = remove_commitment(e, dst);
+    if (dst == kPoolCommon) {
+      release_idle_one(src, e);
+      return;
+    }
+    goto_stage(e, pool_stage(dst));
+  }
+
+  __device__ void fulfill_from_source() {  // :730-743
+    int32_t* idle = S<int32_t>(O.sc_keys_a);
+    int32_t* plan = S<int32_t>(O.sc_plan);
+    const int n_idle = idle_order(h.source, idle);
+    const int n_plan = h.source >= 0 ? commit_plan(h.source, plan) : 0;
+    int k = 0;
+    for (int c = 0; c < n_plan; ++c) {
+      const int dst = plan[2 * c];
+      int n = plan[2 * c + 1];
+      check(dst >= 0 && n > 0);
+      while (n > 0 && k < n_idle && !frozen()) {
+        const int e = idle[k++];
+        fulfill(e, dst);
+        n--;
+      }
+    }
+    check(k == n_idle);
+  }
+
+  __device__ void commit_leftovers() {  // :487-503
+    const int n = committable();
+    if (n > 0) add_commitment(n, kPoolCommon);
+  }
+
+  __device__ bool release(int e, int g, bool changed) {  // _handle_released_executor :639-660
+    const int dst = peek_commitment(stage_pool(g));
+    if (dst != kPoolNone) {
+      fulfill(e, dst);
+      return true;
+    }
+    ex_task(e) = -1;
+    if (changed) release_idle_one(stage_pool(g), e);
+    return false;
+  }
+
+  // ---------------------------------------------------------------- event handlers (:428-483)
+  __device__ void on_job_arrival(int j) {
+    job_state(j) = kJobActive;
+    job_arr_dec(j) = h.decisions;
+    int32_t* aj = F<int32_t>(O.active_jobs);
+    int32_t* as = F<int32_t>(O.active_stages);
+    if (W::lane() == 0) aj[h.n_active_jobs] = j;
+    const int base = job_base(j), n = job_nst(j);
+    for (int k0 = 0; k0 <= n; k0 += W::kWidth) {  // pools of the job and its stages, active-stage list
+      const int k = k0 + W::lane();
+      if (k <= n) {
+        const int p = (k == n) ? job_pool(j) : stage_pool(base + k);
+        ps_init(pmeta(p), ptab(p));
+        cfrom(p) = 0;
+        if (k < n) as[h.n_active_stages + k] = base + k;
+      }
+    }
+    W::sync();
+    h.n_active_jobs += 1;
+    h.n_active_stages += n;
+    if (pool_size(kPoolCommon) > 0) h.source = kPoolCommon;
+  }
+
+  __device__ void on_executor_arrival(int e, int g) {  // :440-450
+    const int j = st_job(g);
+    check(ex_task(e) < 0);  // Job.attach_executor asserts executor.task is None
+    job_local(j) += 1;
+    ex_job(e) = j;
+    st_mov(g) -= 1;
+    check(st_mov(g) >= 0);
+    move_to_pool(e, job_pool(j), false);
+    goto_stage(e, g);
+  }
+
+  __device__ bool stage_completed(int j, int g) {  // Job.record_stage_completion (job.py:65-73,113-128)
+    check(st_unmet(g) == 0);  // frontier_stages.remove(stage)
+    list_remove(F<int32_t>(O.active_stages), h.n_active_stages, g);
+    h.n_active_stages -= 1;
+    job_nact(j) -= 1;
+    const int ts = st_ts(g), base = job_base(j);
+    bool changed = false;
+    for (int k = D.ts_child_base[ts]; k < D.ts_child_base[ts + 1]; ++k) {
+      const int c = base + D.ts_children[k];
+      st_unmet(c) -= 1;
+      if (st_unmet(c) == 0 && !st_completed(c)) changed = true;
+    }
+    return changed;
+  }
+
+  __device__ void job_completed(int j) {  // :682-697
+    if (pool_size(job_pool(j)) > 0) release_idle_all(job_pool(j));
+    check(pool_size(job_pool(j)) == 0);
+    list_remove(F<int32_t>(O.active_jobs), h.n_active_jobs, j);
+    h.n_active_jobs -= 1;
+    h.n_completed += 1;
+    job_state(j) = kJobDone;
+    job_tdone(j) = h.wall;
+    job_done_dec(j) = h.decisions;
+    trace(h.wall, kTrJobDone, -1, j, -1, -1);
+  }
+
+  __device__ void on_task_done(int e, int g) {  // :452-483
+    const int j = st_job(g);
+    check(!st_completed(g));
+    st_exe(g) -= 1;
+    st_done(g) += 1;
+    ex_busy(e) = 0;
+    if (st_rem(g) > 0) {
+      run_next_task(e, g);
+      return;
+    }
+    bool changed = false;
+    if (st_completed(g)) changed = stage_completed(j, g);
+    if (job_nact(j) == 0) job_completed(j);
+    const bool had = release(e, g, changed);
+    if (changed)
+      h.source = job_pool(j);
+    else if (!had)
+      h.source = stage_pool(g);
+  }
+
+  // Pops the min (t, seq) event: arrival cursor vs. per-executor slots. Returns false when empty.
+  __device__ bool pop_event(double* t, int* kind, int* e, int* g, int* seq) {
+    double bt = 0.0;
+    int bseq = 0x7FFFFFFF, be = -1;
+    for (int k0 = 0; k0 < L.num_executors; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      const bool ok = k < L.num_executors && ev_seq(k) >= 0;
+      double tt = ok ? ev_t(k) : __builtin_inf();
+      int ss = ok ? ev_seq(k) : 0x7FFFFFFF;
+      int kk = ok ? k : -1;
+      W::min_event(tt, ss, kk);
+      if (kk >= 0 && (be < 0 || tt < bt || (tt == bt && ss < bseq))) {
+        bt = tt;
+        bseq = ss;
+        be = kk;
+      }
+    }
+    const bool have_arr = h.arrivals < h.num_jobs;
+    if (have_arr) {
+      const double ta = job_tarr(h.arrivals);
+      const int sa = h.arrivals;  // arrivals were pushed first with seq 0..J-1
+      if (be < 0 || ta < bt || (ta == bt && sa < bseq)) {
+        *t = ta;
+        *kind = kEvArrival;
+        *e = -1;
+        *g = h.arrivals;  // job id
+        *seq = sa;
+        h.arrivals++;
+        return true;
+      }
+    }
+    if (be < 0) return false;
+    *t = bt;
+    *kind = ev_type(be);
+    *e = be;
+    *g = ev_stage(be);
+    *seq = bseq;
+    ev_seq(be) = -1;
+    return true;
+  }
+
+  __device__ void simulate() {  // _resume_simulation :320-343
+    h.step_events = 0;
+    for (;;) {
+      if (frozen()) return;
+      double t;
+      int kind, e, g, seq;
+      if (!pop_event(&t, &kind, &e, &g, &seq)) return;
+      h.wall = t;
+      h.events++;
+      h.step_events++;
+      if (kind == kEvArrival) {
+        trace(t, kind, -1, g, -1, seq);
+        on_job_arrival(g);
+      } else {
+        const int j = st_job(g);
+        trace(t, kind, e, j, g - job_base(j), seq);
+        if (kind == kEvReady)
+          on_executor_arrival(e, g);
+        else
+          on_task_done(e, g);
+      }
+      if (committable() == 0) continue;
+      if (any_schedulable()) return;
+      release_idle_all(kPoolNone);
+      h.source = kPoolNone;
+    }
+  }
+
+  __device__ double jobtime(double t0, int dec) {  // _compute_jobtime :847-874
+    const double span = h.wall - t0;
+    if (span == 0.0) return 0.0;
+    double part = 0.0;
+    for (int j0 = 0; j0 < h.arrivals; j0 += W::kWidth) {
+      const int j = j0 + W::lane();
+      if (j < h.arrivals) {
+        const int st = job_state(j);
+        const bool in_union =
+            st == kJobActive || (st == kJobDone && job_done_dec(j) == dec && job_arr_dec(j) < dec);
+        if (in_union) {
+          const double ta = job_tarr(j);
+          const double a = ta > t0 ? ta : t0;
+          const double tc = st == kJobDone ? job_tdone(j) : h.wall;
+          const double b = tc < h.wall ? tc : h.wall;
+          if (C.beta == 0.0)
+            part += b - a;
+          else
+            part += exp(-C.beta * 1e-3 * (a - t0)) - exp(-C.beta * 1e-3 * (b - t0));
+        }
+      }
+    }
+    double total = W::sum_d(part);
+    if (C.beta > 0.0) total /= C.beta;
+    return total;
+  }
+
+  // ---------------------------------------------------------------- observation (:345-406, utils.py)
+  __device__ void observe(double reward) {
+    const int n = h.n_active_stages;
+    const int src_job = source_job();
+    const int32_t* act = F<int32_t>(O.active_stages);
+    int32_t* sched = F<int32_t>(O.sched_list);
+    int32_t* row_of = S<int32_t>(O.sc_row_of);
+    float* nodes = reinterpret_cast<float*>(obs + L.ob_nodes) + (int64_t)eid * L.stage_cap * 3;
+    uint8_t* front = obs + L.ob_frontier + (int64_t)eid * L.stage_cap;
+    int32_t* srank = reinterpret_cast<int32_t*>(obs + L.ob_sched_rank) + (int64_t)eid * L.stage_cap;
+    int nsched = 0;
+    for (int i0 = 0; i0 < n; i0 += W::kWidth) {
+      const int i = i0 + W::lane();
+      const bool ok = i < n;
+      const int g = ok ? act[i] : -1;
+      const bool s = ok && stage_pred(g, kScanAll, -1, src_job);
+      const uint64_t m = W::ballot(s);
+      const int r = nsched + W::rank(m);
+      if (ok) {
+        nodes[3 * i + 0] = (float)st_rem(g);
+        nodes[3 * i + 1] = (float)st_recent(g);
+        nodes[3 * i + 2] = s ? 1.0f : 0.0f;
+        front[i] = st_unmet(g) == 0 ? 1 : 0;
+        srank[i] = s ? r : -1;
+        row_of[g] = i;
+        if (s) sched[r] = g;
+      }
+      nsched += W::popc(m);
+    }
+    W::sync();
+    // jobs: dag_ptr, exec_supplies, source_job_idx
+    const int nj = h.n_active_jobs;
+    const int32_t* aj = F<int32_t>(O.active_jobs);
+    int32_t* ptr = reinterpret_cast<int32_t*>(obs + L.ob_dag_ptr) + (int64_t)eid * (L.job_cap + 1);
+    int32_t* sup = reinterpret_cast<int32_t*>(obs + L.ob_supplies) + (int64_t)eid * L.job_cap;
+    int src_idx = nj, run = 0;
+    for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      const bool ok = k < nj;
+      const int j = ok ? aj[k] : -1;
+      const int cnt = ok ? job_nact(j) : 0;
+      int total = 0;
+      const int ex = W::excl_scan(cnt, &total);
+      if (ok) {
+        ptr[k] = run + ex;
+        sup[k] = job_supply(j);
+      }
+      const uint64_t ms = W::ballot(ok && j == src_job);
+      if (ms) src_idx = k0 + W::ffs(ms);
+      run += total;
+    }
+    if (W::lane() == 0) ptr[nj] = run;
+    check(run == n);
+    // edges: (row(u), row(v)) for active u, child v active; order = node order, children ascending
+    int64_t* links = reinterpret_cast<int64_t*>(obs + L.ob_edge_links) + (int64_t)eid * L.edge_cap * 2;
+    int ne = 0;
+    for (int i0 = 0; i0 < n; i0 += W::kWidth) {
+      const int i = i0 + W::lane();
+      const bool ok = i < n;
+      const int g = ok ? act[i] : -1;
+      int cnt = 0, cb = 0, ce = 0, base = 0;
+      if (ok) {
+        const int ts = st_ts(g);
+        base = job_base(st_job(g));
+        cb = D.ts_child_base[ts];
+        ce = D.ts_child_base[ts + 1];
+        for (int k = cb; k < ce; ++k)
+          if (!st_completed(base + D.ts_children[k])) cnt++;
+      }
+      int total = 0;
+      const int ex = W::excl_scan(cnt, &total);
+      if (ok) {
+        int o = ne + ex;
+        for (int k = cb; k < ce; ++k) {
+          const int c = base + D.ts_children[k];
+          if (!st_completed(c) && o < L.edge_cap) {
+            links[2 * o + 0] = i;
+            links[2 * o + 1] = row_of[c];
+            o++;
+          }
+        }
+      }
+      ne += total;
+    }
+    if (ne > L.edge_cap) fail(SSIM_ERR_CAPACITY);
+    h.n_sched = nsched;
+    h.stage_idx_n = n + 1;
+    h.acc_nodes += n;
+    h.acc_edges += ne;
+    h.acc_jobs += nj;
+    h.acc_events += h.step_events;
+    W::sync();
+    if (W::lane() == 0) {
+      int64_t* acc = reinterpret_cast<int64_t*>(obs + L.ob_acc) + (int64_t)eid * 4;
+      acc[0] = h.acc_nodes;
+      acc[1] = h.acc_edges;
+      acc[2] = h.acc_jobs;
+      acc[3] = h.acc_events;
+      int32_t* cnts = reinterpret_cast<int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
+      cnts[SSIM_OC_NUM_NODES] = n;
+      cnts[SSIM_OC_NUM_EDGES] = ne;
+      cnts[SSIM_OC_NUM_JOBS] = nj;
+      cnts[SSIM_OC_COMMITTABLE] = committable();
+      cnts[SSIM_OC_SOURCE_JOB_IDX] = src_idx;
+      cnts[SSIM_OC_NUM_SCHEDULABLE] = nsched;
+      cnts[SSIM_OC_TERMINATED] = h.terminated;
+      cnts[SSIM_OC_TRUNCATED] = h.wall >= h.time_limit ? 1 : 0;
+      cnts[SSIM_OC_ERR] = (int32_t)h.err;
+      cnts[SSIM_OC_DECISIONS] = h.decisions;
+      cnts[SSIM_OC_EVENTS] = h.events;
+      cnts[SSIM_OC_NUM_COMPLETED] = h.n_completed;
+      cnts[SSIM_OC_NUM_ARRIVED] = h.arrivals;
+      cnts[SSIM_OC_TRACE_LEN] = h.trace_len;
+      cnts[SSIM_OC_STEP_EVENTS] = h.step_events;
+      cnts[SSIM_OC_EPISODE] = h.episode;
+      reinterpret_cast<double*>(obs + L.ob_reward)[eid] = reward;
+      reinterpret_cast<double*>(obs + L.ob_wall_time)[eid] = h.wall;
+    }
+    W::sync();
+  }
+
+  __device__ void write_err_only(uint32_t transient) {
+    W::sync();
+    if (W::lane() == 0) {
+      int32_t* cnts = reinterpret_cast<int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
+      cnts[SSIM_OC_ERR] = (int32_t)(h.err | transient);
+    }
+    W::sync();
+  }
+
+  // ---------------------------------------------------------------- step (:188-221, :275-315)
+  __device__ void step(StepIn a) {
+    load_header();
+    if (h.terminated || frozen() || h.num_jobs == 0) return;
+    const int idx = a.stage_idx, nx = a.num_exec;
+    // Discrete(n, start=-1) holds -1 .. n-2; Discrete(N, start=1) holds 1 .. N
+    if (idx < -1 || idx > h.stage_idx_n - 2 || nx < 1 || nx > L.num_executors) {
+      write_err_only(SSIM_ERR_SPACE);
+      return;
+    }
+    if (idx == -1) {
+      commit_leftovers();
+    } else {
+      if (idx >= h.n_sched) {
+        write_err_only(SSIM_ERR_KEY);
+        return;
+      }
+      const int g = F<int32_t>(O.sched_list)[idx];
+      if (nx > committable()) {
+        write_err_only(SSIM_ERR_TOO_MANY);
+        return;
+      }
+      const int d = demand(g);
+      const int n = nx < d ? nx : d;  // _adjust_num_executors
+      check(n > 0);
+      add_commitment(n, stage_pool(g));
+      st_sel(g) = 1;
+      if (W::lane() == 0) F<int32_t>(O.sel_list)[h.n_selected] = g;
+      h.n_selected++;
+      W::sync();
+    }
+    h.decisions++;
+    h.step_events = 0;
+    if (committable() > 0 && any_schedulable()) {
+      observe(0.0);
+      store_header();
+      return;
+    }
+    commit_leftovers();
+    fulfill_from_source();
+    h.source = kPoolNone;
+    {  // selected_stages.clear()
+      const int32_t* sl = F<int32_t>(O.sel_list);
+      for (int k0 = 0; k0 < h.n_selected; k0 += W::kWidth) {
+        const int k = k0 + W::lane();
+        if (k < h.n_selected) st_sel(sl[k]) = 0;
+      }
+      h.n_selected = 0;
+      W::sync();
+    }
+    const double t0 = h.wall;
+    simulate();
+    const double reward = -jobtime(t0, h.decisions);
+    h.terminated = (h.n_completed == h.num_jobs) ? 1 : 0;
+    if (!h.terminated) check(committable() > 0 && any_schedulable());
+    observe(reward);
+    store_header();
+  }
+
+  // ---------------------------------------------------------------- reset (:127-186, :260-273)
+  __device__ void reset(const uint8_t* rec_base) {
+    const ssim_reset_record* rec = reinterpret_cast<const ssim_reset_record*>(rec_base);
+    const double* tarr = reinterpret_cast<const double*>(rec_base + kResetHeadBytes);
+    const int32_t* tpl = reinterpret_cast<const int32_t*>(rec_base + kResetHeadBytes + 8 * (int64_t)L.job_cap);
+    const int nj = rec->num_jobs;
+    if (nj <= 0) return;
+    const int prev_episode = F<EnvHeader>(O.hdr)->episode;
+    EnvHeader z;
+    memset(&z, 0, sizeof(z));
+    h = z;
+    h.episode = prev_episode + 1;
+    h.time_limit = rec->time_limit;
+    rng.s_hi = rec->rng_state_hi;
+    rng.s_lo = rec->rng_state_lo;
+    rng.i_hi = rec->rng_inc_hi;
+    rng.i_lo = rec->rng_inc_lo;
+    rng.has32 = rec->rng_has_uint32;
+    rng.u32 = rec->rng_uinteger;
+    h.num_jobs = nj;
+    h.seq = nj;
+    h.source = kPoolCommon;
+    h.commit_seq = 0;
+    if (nj > L.job_cap) {
+      fail(SSIM_ERR_RESET);
+      h.num_jobs = 0;
+      observe(0.0);
+      store_header();
+      return;
+    }
+    // jobs: template, stage base (exclusive scan of stage counts)
+    int run = 0;
+    bool bad = false;
+    for (int j0 = 0; j0 < nj; j0 += W::kWidth) {
+      const int j = j0 + W::lane();
+      const bool ok = j < nj;
+      const int t = ok ? tpl[j] : 0;
+      const bool tb = ok && (t < 0 || t >= D.num_templates);
+      const int ns = (ok && !tb) ? D.tpl_stage_base[t + 1] - D.tpl_stage_base[t] : 0;
+      int total = 0;
+      const int ex = W::excl_scan(ns, &total);
+      if (ok) {
+        job_tpl(j) = t;
+        job_base(j) = run + ex;
+        job_nst(j) = ns;
+        job_nact(j) = ns;
+        job_sat(j) = 0;
+        job_local(j) = 0;
+        job_supply(j) = 0;
+        job_state(j) = kJobPending;
+        job_arr_dec(j) = -1;
+        job_done_dec(j) = -1;
+        job_tarr(j) = tarr[j];
+        job_tdone(j) = __builtin_inf();
+      }
+      if (W::ballot(tb)) bad = true;
+      run += total;
+    }
+    if (bad || run > L.stage_cap) {
+      fail(SSIM_ERR_RESET);
+      h.num_jobs = 0;
+      observe(0.0);
+      store_header();
+      return;
+    }
+    W::sync();
+    // stages
+    for (int j = 0; j < nj; ++j) {
+      const int t = job_tpl(j), base = job_base(j), ns = job_nst(j), tsb = D.tpl_stage_base[t];
+      for (int k0 = 0; k0 < ns; k0 += W::kWidth) {
+        const int k = k0 + W::lane();
+        if (k < ns) {
+          const int g = base + k, ts = tsb + k;
+          st_job(g) = j;
+          st_ts(g) = ts;
+          st_rem(g) = D.ts_num_tasks[ts];
+          st_exe(g) = 0;
+          st_done(g) = 0;
+          st_mov(g) = 0;
+          st_com(g) = 0;
+          st_unmet(g) = D.ts_parent_base[ts + 1] - D.ts_parent_base[ts];
+          st_sel(g) = 0;
+          st_recent(g) = D.ts_rough[ts];
+        }
+      }
+    }
+    // executors, commitments, COMMON pool = set(range(N))
+    for (int k0 = 0; k0 < L.num_executors; k0 += W::kWidth) {
+      const int e = k0 + W::lane();
+      if (e < L.num_executors) {
+        ex_loc(e) = kPoolCommon;
+        ex_job(e) = -1;
+        ex_task(e) = -1;
+        ex_busy(e) = 0;
+        ev_seq(e) = -1;
+        ev_t(e) = 0.0;
+        ev_type(e) = 0;
+        ev_stage(e) = -1;
+      }
+    }
+    for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      if (k < L.commit_cap) F<int32_t>(O.cm_cnt)[k] = 0;
+    }
+    W::sync();
+    if (W::lane() == 0) {
+      ps_init(pmeta(kPoolCommon), ptab(kPoolCommon));
+      for (int e = 0; e < L.num_executors; ++e)
+        ps_add(pmeta(kPoolCommon), ptab(kPoolCommon), (uint32_t)e, S<int32_t>(O.sc_keys_b));
+    }
+    cfrom(kPoolCommon) = 0;
+    W::sync();
+    // _load_initial_jobs: arrivals with t <= 0 (wall_time stays 0)
+    while (h.arrivals < h.num_jobs && job_tarr(h.arrivals) <= 0.0) {
+      const int j = h.arrivals++;
+      h.events++;
+      trace(0.0, kEvArrival, -1, j, -1, j);
+      on_job_arrival(j);
+    }
+    if (h.num_jobs > 0) check(job_tarr(0) == 0.0);  // "first job must arrive at t=0"
+    observe(0.0);
+    store_header();
+  }
+};
+
+}  // namespace ssim

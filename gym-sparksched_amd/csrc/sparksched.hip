@@ -1,0 +1,259 @@
+// sparksched.hip — gfx950 kernels and the C ABI (include/sparksched.h).
+//
+// One 64-lane wavefront per env (one workgroup = one wave; no workgroup barriers needed). Per-env state
+// lives in the caller's state arena in HBM (env-major SoA, layout.h); per-launch scratch (node row map,
+// temporary CPython-set tables, commitment plan) lives in LDS. Kernels:
+//   k_reset   : env init from a host-sampled job sequence + _load_initial_jobs + first observation
+//   k_step    : one env.step per env from device action arrays (obs written to the obs arena)
+//   k_policy  : device action driver (fair / FIFO / random) reading the obs arena
+//   k_rollout : `num_steps` x (policy -> step) fused into one launch (no host round trips)
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "sparksched.h"
+#include "engine.h"
+#include "policy.h"
+
+using namespace ssim;
+
+// ------------------------------------------------------------------------------------------ wave ops
+struct WaveHip {
+  static constexpr int kWidth = 64;
+  __device__ static __forceinline__ int lane() { return (int)__lane_id(); }
+  __device__ static __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
+  __device__ static __forceinline__ int ffs(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
+  __device__ static __forceinline__ int popc(uint64_t m) { return __popcll((unsigned long long)m); }
+  __device__ static __forceinline__ int rank(uint64_t m) {  // set bits of m below this lane
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  }
+  __device__ static __forceinline__ int bcast_i(int v, int l) { return __shfl(v, l); }
+  __device__ static __forceinline__ void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ static __forceinline__ int excl_scan(int x, int* total) {
+    int v = x;
+    const int l = lane();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(v, (unsigned)off);
+      if (l >= off) v += y;
+    }
+    *total = __shfl(v, 63);
+    return v - x;
+  }
+  __device__ static __forceinline__ double sum_d(double x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    return x;
+  }
+  // lexicographic min of (key, val) across the wave, result in every lane
+  __device__ static __forceinline__ void min_pair(int& key, int& val) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const int k2 = __shfl_xor(key, off), v2 = __shfl_xor(val, off);
+      if (k2 < key || (k2 == key && v2 < val)) {
+        key = k2;
+        val = v2;
+      }
+    }
+  }
+  // min of (t, seq) with payload idx across the wave
+  __device__ static __forceinline__ void min_event(double& t, int& seq, int& idx) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double t2 = __shfl_xor(t, off);
+      const int s2 = __shfl_xor(seq, off), i2 = __shfl_xor(idx, off);
+      if (t2 < t || (t2 == t && s2 < seq)) {
+        t = t2;
+        seq = s2;
+        idx = i2;
+      }
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------ kernels
+extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
+
+__global__ __launch_bounds__(64) void k_reset(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+                                              const uint8_t* __restrict__ reset) {
+  const int eid = blockIdx.x;
+  Sim<WaveHip> s(P, state, g_smem, obs, eid);
+  s.reset(reset + (int64_t)eid * P->L.reset_stride);
+}
+
+__global__ __launch_bounds__(64) void k_step(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+                                             const int32_t* __restrict__ stage_idx,
+                                             const int32_t* __restrict__ num_exec) {
+  const int eid = blockIdx.x;
+  Sim<WaveHip> s(P, state, g_smem, obs, eid);
+  StepIn a;
+  a.stage_idx = stage_idx[eid];
+  a.num_exec = num_exec[eid];
+  s.step(a);
+}
+
+__global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, const uint8_t* obs, int kind,
+                                               uint64_t seed, uint64_t counter, int32_t* stage_idx,
+                                               int32_t* num_exec) {
+  const int eid = blockIdx.x;
+  PolicyView<WaveHip> v{P->L, obs, eid};
+  const StepIn a = v.act(kind, seed, counter);
+  if (WaveHip::lane() == 0) {
+    stage_idx[eid] = a.stage_idx;
+    num_exec[eid] = a.num_exec;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+                                                int kind, uint64_t seed, int num_steps, int32_t* action_log) {
+  const int eid = blockIdx.x;
+  const int B = P->L.num_envs;
+  Sim<WaveHip> s(P, state, g_smem, obs, eid);
+  PolicyView<WaveHip> v{P->L, obs, eid};
+  for (int k = 0; k < num_steps; ++k) {
+    const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.env + P->O.hdr);
+    const StepIn a = v.act(kind, seed, (uint64_t)hd->decisions + ((uint64_t)hd->episode << 32));
+    if (action_log != nullptr && WaveHip::lane() == 0) {
+      action_log[((int64_t)k * B + eid) * 2 + 0] = a.stage_idx;
+      action_log[((int64_t)k * B + eid) * 2 + 1] = a.num_exec;
+    }
+    WaveHip::sync();
+    s.step(a);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ C ABI
+struct ssim_handle {
+  Params params;  // host copy (device copy at the start of the state arena)
+  uint8_t* state;
+  uint8_t* obs;
+  uint8_t* reset;
+};
+
+static thread_local char g_err[512] = "";
+
+static int set_err(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+static int hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) return set_err(SSIM_E_HIP, "%s: %s", what, hipGetErrorString(e));
+  return SSIM_OK;
+}
+
+static const int64_t kMaxDynLds = 64 * 1024;
+
+extern "C" int ssim_layout_for(const ssim_config* cfg, ssim_layout* out) {
+  StateOffsets O;
+  if (cfg == nullptr || out == nullptr || !compute_layout(*cfg, out, &O))
+    return set_err(SSIM_E_ARG, "ssim_layout_for: invalid config");
+  return SSIM_OK;
+}
+
+extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, void* state_arena,
+                           void* obs_arena, void* reset_arena, ssim_handle** out) {
+  if (cfg == nullptr || dataset == nullptr || state_arena == nullptr || obs_arena == nullptr ||
+      reset_arena == nullptr || out == nullptr)
+    return set_err(SSIM_E_ARG, "ssim_create: null argument");
+  ssim_handle* h = new ssim_handle();
+  if (!compute_layout(*cfg, &h->params.L, &h->params.O)) {
+    delete h;
+    return set_err(SSIM_E_ARG, "ssim_create: invalid config");
+  }
+  if (h->params.L.scratch_bytes > kMaxDynLds) {
+    delete h;
+    return set_err(SSIM_E_ARG, "ssim_create: per-env scratch %lld B exceeds LDS budget",
+                   (long long)h->params.L.scratch_bytes);
+  }
+  h->params.D = *dataset;
+  h->params.C = *cfg;
+  h->state = static_cast<uint8_t*>(state_arena);
+  h->obs = static_cast<uint8_t*>(obs_arena);
+  h->reset = static_cast<uint8_t*>(reset_arena);
+  int rc = hip_check(hipMemcpy(h->state, &h->params, sizeof(Params), hipMemcpyHostToDevice), "params upload");
+  if (rc == SSIM_OK) rc = hip_check(hipMemset(h->obs, 0, (size_t)h->params.L.obs_bytes), "obs clear");
+  if (rc == SSIM_OK)
+    rc = hip_check(hipMemset(h->state + kParamsReserve, 0, (size_t)(h->params.L.state_bytes - kParamsReserve)),
+                   "state clear");
+  if (rc != SSIM_OK) {
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return SSIM_OK;
+}
+
+extern "C" int ssim_destroy(ssim_handle* h) {
+  delete h;
+  return SSIM_OK;
+}
+
+static const Params* dparams(const ssim_handle* h) { return reinterpret_cast<const Params*>(h->state); }
+
+extern "C" int ssim_reset(ssim_handle* h, void* stream) {
+  if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_reset: null handle");
+  const ssim_layout& L = h->params.L;
+  hipLaunchKernelGGL(k_reset, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
+                     dparams(h), h->state, h->obs, h->reset);
+  return hip_check(hipGetLastError(), "k_reset launch");
+}
+
+extern "C" int ssim_step(ssim_handle* h, const int32_t* stage_idx, const int32_t* num_exec, void* stream) {
+  if (h == nullptr || stage_idx == nullptr || num_exec == nullptr) return set_err(SSIM_E_ARG, "ssim_step: null");
+  const ssim_layout& L = h->params.L;
+  hipLaunchKernelGGL(k_step, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
+                     dparams(h), h->state, h->obs, stage_idx, num_exec);
+  return hip_check(hipGetLastError(), "k_step launch");
+}
+
+extern "C" int ssim_policy(ssim_handle* h, int32_t kind, uint64_t seed, uint64_t counter, int32_t* stage_idx,
+                           int32_t* num_exec, void* stream) {
+  if (h == nullptr || stage_idx == nullptr || num_exec == nullptr) return set_err(SSIM_E_ARG, "ssim_policy: null");
+  if (kind != SSIM_POLICY_FAIR && kind != SSIM_POLICY_FIFO && kind != SSIM_POLICY_RANDOM)
+    return set_err(SSIM_E_ARG, "ssim_policy: unknown policy %d", kind);
+  const ssim_layout& L = h->params.L;
+  hipLaunchKernelGGL(k_policy, dim3(L.num_envs), dim3(64), 0, (hipStream_t)stream, dparams(h), h->obs, kind,
+                     seed, counter, stage_idx, num_exec);
+  return hip_check(hipGetLastError(), "k_policy launch");
+}
+
+extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t* action_log,
+                            void* stream) {
+  if (h == nullptr || num_steps < 0) return set_err(SSIM_E_ARG, "ssim_rollout: bad argument");
+  if (kind != SSIM_POLICY_FAIR && kind != SSIM_POLICY_FIFO && kind != SSIM_POLICY_RANDOM)
+    return set_err(SSIM_E_ARG, "ssim_rollout: unknown policy %d", kind);
+  const ssim_layout& L = h->params.L;
+  hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
+                     dparams(h), h->state, h->obs, kind, seed, num_steps, action_log);
+  return hip_check(hipGetLastError(), "k_rollout launch");
+}
+
+extern "C" int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32_t* state, void* stream) {
+  if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_job_times: null handle");
+  const ssim_layout& L = h->params.L;
+  const StateOffsets& O = h->params.O;
+  const size_t J = (size_t)L.job_cap, B = (size_t)L.num_envs, pitch = (size_t)L.env_bytes;
+  const uint8_t* base = h->state + kParamsReserve;
+  hipStream_t s = (hipStream_t)stream;
+  int rc = SSIM_OK;
+  if (t_arrival)
+    rc = hip_check(hipMemcpy2DAsync(t_arrival, J * 8, base + O.job_tarr, pitch, J * 8, B, hipMemcpyDeviceToDevice, s),
+                   "job t_arrival copy");
+  if (rc == SSIM_OK && t_completed)
+    rc = hip_check(hipMemcpy2DAsync(t_completed, J * 8, base + O.job_tdone, pitch, J * 8, B, hipMemcpyDeviceToDevice, s),
+                   "job t_completed copy");
+  if (rc == SSIM_OK && state)
+    rc = hip_check(hipMemcpy2DAsync(state, J * 4, base + O.job_state, pitch, J * 4, B, hipMemcpyDeviceToDevice, s),
+                   "job state copy");
+  return rc;
+}
+
+extern "C" const char* ssim_last_error(void) { return g_err; }

@@ -1,0 +1,94 @@
+"""ctypes mirror of include/sparksched.h (plain C structs; shared by the device library loader)."""
+
+from __future__ import annotations
+
+import ctypes as ct
+
+SSIM_ERR_SPACE = 0x1
+SSIM_ERR_KEY = 0x2
+SSIM_ERR_TOO_MANY = 0x4
+SSIM_ERR_INVARIANT = 0x10
+SSIM_ERR_CAPACITY = 0x20
+SSIM_ERR_SAMPLER = 0x40
+SSIM_ERR_RESET = 0x80
+SSIM_ERR_STICKY = 0xF0
+
+SSIM_POLICY_FAIR = 1
+SSIM_POLICY_FIFO = 2
+SSIM_POLICY_RANDOM = 3
+
+# indices into the per-env int32 counts block
+OC_NUM_NODES, OC_NUM_EDGES, OC_NUM_JOBS, OC_COMMITTABLE, OC_SOURCE_JOB_IDX, OC_NUM_SCHEDULABLE = range(6)
+OC_TERMINATED, OC_TRUNCATED, OC_ERR, OC_DECISIONS, OC_EVENTS, OC_NUM_COMPLETED = range(6, 12)
+OC_NUM_ARRIVED, OC_TRACE_LEN, OC_STEP_EVENTS, OC_EPISODE = range(12, 16)
+NUM_COUNTS = 16
+RESET_HEAD_BYTES = 64
+TRACE_BYTES = 32
+
+
+class SsimConfig(ct.Structure):
+    _fields_ = [
+        ("num_envs", ct.c_int32),
+        ("num_executors", ct.c_int32),
+        ("job_cap", ct.c_int32),
+        ("max_stages", ct.c_int32),
+        ("max_edges", ct.c_int32),
+        ("trace_cap", ct.c_int32),
+        ("moving_delay", ct.c_double),
+        ("warmup_delay", ct.c_double),
+        ("beta", ct.c_double),
+    ]
+
+
+class SsimDataset(ct.Structure):
+    _fields_ = [
+        ("num_templates", ct.c_int32),
+        ("num_template_stages", ct.c_int32),
+        ("tpl_stage_base", ct.c_void_p),
+        ("ts_num_tasks", ct.c_void_p),
+        ("ts_rough", ct.c_void_p),
+        ("ts_child_base", ct.c_void_p),
+        ("ts_children", ct.c_void_p),
+        ("ts_parent_base", ct.c_void_p),
+        ("ts_parents", ct.c_void_p),
+        ("ts_fw_keymask", ct.c_void_p),
+        ("ts_fw_maxlevel", ct.c_void_p),
+        ("dur_off", ct.c_void_p),
+        ("dur_len", ct.c_void_p),
+        ("durations", ct.c_void_p),
+        ("intervals", ct.c_void_p),
+    ]
+
+
+# order of the pointer fields above = order of arrays in PackedDataset.arrays()
+DATASET_ARRAYS = [
+    "tpl_stage_base", "ts_num_tasks", "ts_rough", "ts_child_base", "ts_children", "ts_parent_base",
+    "ts_parents", "ts_fw_keymask", "ts_fw_maxlevel", "dur_off", "dur_len", "durations", "intervals",
+]
+
+
+class SsimResetRecord(ct.Structure):
+    _fields_ = [
+        ("rng_state_hi", ct.c_uint64),
+        ("rng_state_lo", ct.c_uint64),
+        ("rng_inc_hi", ct.c_uint64),
+        ("rng_inc_lo", ct.c_uint64),
+        ("rng_has_uint32", ct.c_uint32),
+        ("rng_uinteger", ct.c_uint32),
+        ("num_jobs", ct.c_int32),
+        ("pad", ct.c_int32),
+        ("time_limit", ct.c_double),
+    ]
+
+
+class SsimLayout(ct.Structure):
+    _fields_ = [(n, ct.c_int32) for n in (
+        "num_envs", "num_executors", "job_cap", "stage_cap", "edge_cap", "pool_cap", "set_cap", "commit_cap",
+        "trace_cap", "pad0")] + [(n, ct.c_int64) for n in (
+        "env_bytes", "state_bytes", "obs_bytes", "reset_bytes", "reset_stride", "scratch_bytes",
+        "ob_nodes", "ob_edge_links", "ob_dag_ptr", "ob_supplies", "ob_frontier", "ob_sched_rank", "ob_counts",
+        "ob_reward", "ob_wall_time", "ob_acc", "ob_trace")]
+
+
+def layout_dict(layout: SsimLayout) -> dict:
+    return {name: getattr(layout, name) for name, _ in SsimLayout._fields_}

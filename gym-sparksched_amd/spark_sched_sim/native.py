@@ -1,0 +1,52 @@
+"""Loader for the in-tree gfx950 library (libsparksched.so). Fails loudly: there is no CPU fallback."""
+
+from __future__ import annotations
+
+import ctypes as ct
+import os
+
+from ._abi import SsimConfig, SsimDataset, SsimLayout
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "libsparksched.so")
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib() -> ct.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"libsparksched.so not found at {LIB_PATH}; build it with `python __graft_entry__.py build` "
+            "(hipcc --offload-arch=gfx950). The simulator has no CPU fallback.")
+    L = ct.CDLL(LIB_PATH)
+    vp, i32, u64 = ct.c_void_p, ct.c_int32, ct.c_uint64
+    L.ssim_layout_for.argtypes = [ct.POINTER(SsimConfig), ct.POINTER(SsimLayout)]
+    L.ssim_create.argtypes = [ct.POINTER(SsimConfig), ct.POINTER(SsimDataset), vp, vp, vp, ct.POINTER(vp)]
+    L.ssim_destroy.argtypes = [vp]
+    L.ssim_reset.argtypes = [vp, vp]
+    L.ssim_step.argtypes = [vp, vp, vp, vp]
+    L.ssim_policy.argtypes = [vp, i32, u64, u64, vp, vp, vp]
+    L.ssim_rollout.argtypes = [vp, i32, u64, i32, vp, vp]
+    L.ssim_job_times.argtypes = [vp, vp, vp, vp, vp]
+    L.ssim_last_error.restype = ct.c_char_p
+    for name in ("ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
+                 "ssim_rollout", "ssim_job_times"):
+        getattr(L, name).restype = ct.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise NativeError(f"{what} failed ({rc}): {lib().ssim_last_error().decode(errors='replace')}")
+
+
+EXPORTED_SYMBOLS = ["ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
+                    "ssim_rollout", "ssim_job_times", "ssim_last_error"]

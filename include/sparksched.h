@@ -1,0 +1,169 @@
+/*
+ * sparksched.h — C ABI of the MI355X-native batched Spark scheduling simulator.
+ *
+ * Drop-in boundary for the reference's hot path (ArchieGertsman/gym-sparksched, snapshot 2025-02-22):
+ *   SparkSchedSimEnv.reset/step and observation construction
+ *   (spark_sched_sim/spark_sched_sim.py:127-221, 345-406) batched over many independent envs in HBM.
+ *
+ * Conventions: plain C types only (no torch types); every device buffer is caller-allocated device
+ * memory (hipMalloc or a torch tensor); streams are passed as `void*` (hipStream_t, NULL = default).
+ * Every entry point returns 0 on success or a negative SSIM_E_* code, and ssim_last_error() then holds
+ * a message. Per-env failures (invalid action, reference assertion, capacity) do NOT fail the call:
+ * they are reported in the per-env `err` bitmask of the observation arena (SSIM_ERR_* bits).
+ * A handle is not thread-safe; all work is stream-ordered on the caller's stream.
+ */
+#ifndef SPARKSCHED_H
+#define SPARKSCHED_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ------------------------------------------------------------------------------ */
+#define SSIM_OK 0
+#define SSIM_E_ARG -1    /* bad argument / inconsistent sizes */
+#define SSIM_E_HIP -2    /* HIP runtime error (message in ssim_last_error) */
+
+/* ---- per-env error bits (obs arena `err` field) ------------------------------------------------- */
+#define SSIM_ERR_SPACE 0x1u       /* ValueError: action not in action space (spark_sched_sim.py:276-277) */
+#define SSIM_ERR_KEY 0x2u         /* KeyError: stage_idx >= #schedulable stages (spark_sched_sim.py:284) */
+#define SSIM_ERR_TOO_MANY 0x4u    /* ValueError: num_exec > committable executors (:294-295) */
+#define SSIM_ERR_INVARIANT 0x10u  /* an `assert` of the reference fired; env frozen */
+#define SSIM_ERR_CAPACITY 0x20u   /* a device capacity (commitments, trace) overflowed; env frozen */
+#define SSIM_ERR_SAMPLER 0x40u    /* task_duration found no durations (reference raises); env frozen */
+#define SSIM_ERR_RESET 0x80u      /* reset batch inconsistent with the config; env frozen */
+#define SSIM_ERR_STICKY 0xF0u     /* bits that freeze the env until its next reset */
+
+/* ---- device policies (action drivers; schedulers/heuristics) -------------------------------- */
+#define SSIM_POLICY_FAIR 1    /* RoundRobinScheduler(dynamic_partition=True), round_robin.py:14-49 */
+#define SSIM_POLICY_FIFO 2    /* RoundRobinScheduler(dynamic_partition=False) */
+#define SSIM_POLICY_RANDOM 3  /* uniform-random valid action from a counter-based device RNG */
+
+/* Env configuration (spark_sched_sim.py:37-52, tpch.py:19-49). */
+typedef struct ssim_config {
+  int32_t num_envs;
+  int32_t num_executors;  /* N */
+  int32_t job_cap;        /* max jobs per episode (job_arrival_cap, or a bound for time-limited runs) */
+  int32_t max_stages;     /* max stages of any dataset template */
+  int32_t max_edges;      /* max edges of any dataset template */
+  int32_t trace_cap;      /* per-env event-trace records (0 = tracing off) */
+  double moving_delay;    /* ms, spark_sched_sim.py:40 */
+  double warmup_delay;    /* ms, tpch.py:44 */
+  double beta;            /* reward discount, spark_sched_sim.py:44 */
+} ssim_config;
+
+/* Packed TPC-H-format dataset (device pointers). Built on the host from the raw per-query dicts by the
+ * packer, which restates tpch.py:135-206 (preprocessing, num_tasks, rough duration). Template id =
+ * (query_num-1)*7 + size_index. Duration lists: for template-stage ts, wave w (0 fresh_durations,
+ * 1 first_wave(cleaned), 2 rest_wave) and exec level l (EXEC_LEVELS index 0..7):
+ * dur_len[(ts*3+w)*8+l] = -1 if the key is missing, else the list length, at durations[dur_off[...]]. */
+typedef struct ssim_dataset {
+  int32_t num_templates;
+  int32_t num_template_stages;
+  const int32_t* tpl_stage_base;  /* [T+1] */
+  const int32_t* ts_num_tasks;    /* [TS] */
+  const double* ts_rough;         /* [TS] initial most_recent_duration */
+  const int32_t* ts_child_base;   /* [TS+1] CSR into ts_children (local stage ids, ascending) */
+  const int32_t* ts_children;
+  const int32_t* ts_parent_base;  /* [TS+1] CSR into ts_parents */
+  const int32_t* ts_parents;
+  const int32_t* ts_fw_keymask;   /* [TS] bit l set <=> EXEC_LEVELS[l] is a first_wave key */
+  const int32_t* ts_fw_maxlevel;  /* [TS] level index of max(first_wave) */
+  const int32_t* dur_off;         /* [TS*3*8] */
+  const int32_t* dur_len;         /* [TS*3*8] */
+  const double* durations;
+  const double* intervals;        /* [(N+1)*2] executor_intervals (tpch.py:237-262) */
+} ssim_dataset;
+
+/* Per-env reset record (host-sampled job sequence; spark_sched_sim.py:127-186 / tpch.py:54-73).
+ * In the reset arena each env owns `reset_stride` bytes: this record (padded to 64 B), then
+ * double t_arrival[job_cap], then int32 tpl[job_cap] (template id per job, in arrival order). */
+typedef struct ssim_reset_record {
+  uint64_t rng_state_hi, rng_state_lo, rng_inc_hi, rng_inc_lo; /* numpy PCG64 state after sampling */
+  uint32_t rng_has_uint32, rng_uinteger;
+  int32_t num_jobs;    /* 0 = leave this env untouched */
+  int32_t pad;
+  double time_limit;   /* for the `truncated` flag (wrappers/stochastic_time_limit.py:26-31); +inf = none */
+} ssim_reset_record;
+
+/* Sizes and byte offsets. State offsets are within one env's block (stride env_bytes); obs offsets are
+ * absolute within the obs arena, each field strided per env as documented. */
+typedef struct ssim_layout {
+  int32_t num_envs, num_executors, job_cap, stage_cap, edge_cap, pool_cap, set_cap, commit_cap, trace_cap;
+  int32_t pad0;
+  int64_t env_bytes, state_bytes, obs_bytes, reset_bytes, reset_stride, scratch_bytes;
+  /* obs arena (zero-copy views):                                           element   per-env shape   */
+  int64_t ob_nodes;        /* float32  [stage_cap][3]  (remaining, most_recent_duration, schedulable) */
+  int64_t ob_edge_links;   /* int64    [edge_cap][2]   */
+  int64_t ob_dag_ptr;      /* int32    [job_cap+1]     */
+  int64_t ob_supplies;     /* int32    [job_cap]       */
+  int64_t ob_frontier;     /* uint8    [stage_cap]     node has no active parent (heuristics/utils.py:6-8) */
+  int64_t ob_sched_rank;   /* int32    [stage_cap]     schedulable index of node, -1 if not schedulable */
+  int64_t ob_counts;       /* int32    [16]            see SSIM_OC_* */
+  int64_t ob_reward;       /* float64  [1] */
+  int64_t ob_wall_time;    /* float64  [1] */
+  int64_t ob_acc;          /* int64    [4]             running sums of S_act, E_act, J_act, events popped */
+  int64_t ob_trace;       /* float64/int32 trace records, [trace_cap] x 32 B */
+} ssim_layout;
+
+/* indices into the per-env int32 counts block */
+#define SSIM_OC_NUM_NODES 0
+#define SSIM_OC_NUM_EDGES 1
+#define SSIM_OC_NUM_JOBS 2        /* active jobs = len(exec_supplies) */
+#define SSIM_OC_COMMITTABLE 3     /* num_committable_execs */
+#define SSIM_OC_SOURCE_JOB_IDX 4
+#define SSIM_OC_NUM_SCHEDULABLE 5
+#define SSIM_OC_TERMINATED 6
+#define SSIM_OC_TRUNCATED 7
+#define SSIM_OC_ERR 8
+#define SSIM_OC_DECISIONS 9       /* successful env.step calls this episode */
+#define SSIM_OC_EVENTS 10         /* events popped this episode */
+#define SSIM_OC_NUM_COMPLETED 11  /* completed jobs */
+#define SSIM_OC_NUM_ARRIVED 12    /* arrived jobs (completed + active) */
+#define SSIM_OC_TRACE_LEN 13
+#define SSIM_OC_STEP_EVENTS 14    /* events popped by the last step (K of SURVEY §8d) */
+#define SSIM_OC_EPISODE 15
+#define SSIM_NUM_COUNTS 16
+
+typedef struct ssim_handle ssim_handle;
+
+/* Compute all sizes/offsets for a config. No device work. */
+int ssim_layout_for(const ssim_config* cfg, ssim_layout* out);
+
+/* Bind caller-allocated device memory: state arena (layout.state_bytes), obs arena (layout.obs_bytes),
+ * reset staging (layout.reset_bytes). `dataset` holds device pointers and must outlive the handle. */
+int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, void* state_arena, void* obs_arena,
+                void* reset_arena, ssim_handle** out);
+int ssim_destroy(ssim_handle* h);
+
+/* Reset every env whose record in `reset_arena` has num_jobs > 0 (records written by the caller, e.g.
+ * one hipMemcpyAsync of the host-packed buffer). Runs _load_initial_jobs and writes the first obs. */
+int ssim_reset(ssim_handle* h, void* stream);
+
+/* One env.step per env: stage_idx[num_envs], num_exec[num_envs] are device int32 arrays.
+ * Envs that are terminated or frozen are skipped (their obs/flags stay as they are). */
+int ssim_step(ssim_handle* h, const int32_t* stage_idx, const int32_t* num_exec, void* stream);
+
+/* Device action drivers: write stage_idx/num_exec for every env from the current obs. `counter` is the
+ * decision counter mixed into the random policy's counter-based stream. */
+int ssim_policy(ssim_handle* h, int32_t kind, uint64_t seed, uint64_t counter, int32_t* stage_idx,
+                int32_t* num_exec, void* stream);
+
+/* Fused rollout: `num_steps` x (device policy -> step) in ONE launch, obs written every step. The random
+ * policy's counter is (episode << 32) + decisions of each env. `action_log` (optional, device int32
+ * [num_steps][num_envs][2]) receives every action taken, for replay/parity. */
+int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t* action_log,
+                 void* stream);
+
+/* Per-job results for metrics (spark_sched_sim/metrics.py): t_arrival/t_completed float64 [num_envs][job_cap]
+ * and job state int32 [num_envs][job_cap] (0 not arrived, 1 active, 2 completed), any may be NULL. */
+int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32_t* state, void* stream);
+
+const char* ssim_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPARKSCHED_H */

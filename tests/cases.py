@@ -1,0 +1,175 @@
+"""Parity cases shared by the device tests (test_gpu_parity.py, `-m gpu`, gfx950 kernels through the C ABI)
+and the CPU tests of the test-only host build (test_hostsim_parity.py). Each case takes an engine factory
+`make(cfg, B, dataset, trace_cap)` returning a DeviceEngine or HostEngine.
+
+Bit-exact: every observation (float32 node features, int64 edge links, dag_ptr, supplies, committable,
+source index), wall times (float64), terminated flags, decision counts, the full event trace (event order,
+executor assignments, stage/job completions) and job completion times. Rewards within 1e-9 relative.
+"""
+
+import numpy as np
+import pytest
+
+import parity
+from oracle.policies import FairPolicy, RandomPolicy
+from oracle.restatement import SparkSchedOracle
+from spark_sched_sim import _abi
+from spark_sched_sim.engine import decode_trace, obs_dict
+
+LOCKSTEP_CONFIGS = [
+    (dict(beta=5e-3), 4, 7, "random"),
+    (dict(num_executors=50, job_arrival_cap=200, beta=5e-3), 2, 11, "random"),
+    (dict(num_executors=100, job_arrival_cap=200), 1, 21, "fair"),
+    (dict(num_executors=3, job_arrival_cap=20, job_arrival_rate=1e-4, moving_delay=500.0, warmup_delay=100.0),
+     8, 31, "random"),
+]
+
+
+def case_lockstep_fair(make, dataset, env_cfg, B=8, seed0=1234):
+    eng = make(env_cfg, B, dataset, 20000)
+    oracles = [SparkSchedOracle(env_cfg, dataset) for _ in range(B)]
+    steps = parity.run_lockstep(eng, oracles, seeds=[seed0 + i for i in range(B)])
+    assert min(steps) > 100
+    parity.compare_traces(eng, oracles)
+    ta, tc, _ = eng.job_times_np()
+    parity.compare_job_times(ta, tc, oracles)
+
+
+def case_device_fair_policy(make, dataset, env_cfg, B=6):
+    """The on-device RoundRobinScheduler picks exactly the actions of round_robin.py:14-49."""
+    eng = make(env_cfg, B, dataset, 0)
+    oracles = [SparkSchedOracle(env_cfg, dataset) for _ in range(B)]
+    pols = [FairPolicy(env_cfg["num_executors"]) for _ in range(B)]
+    obs = [o.reset(seed=77 + i)[0] for i, o in enumerate(oracles)]
+    eng.reset(seeds=[77 + i for i in range(B)])
+    done = [False] * B
+    for k in range(5000):
+        if all(done):
+            break
+        si, ne = eng.policy(_abi.SSIM_POLICY_FAIR)
+        si, ne = np.array(eng.to_numpy(si)), np.array(eng.to_numpy(ne))
+        for i in range(B):
+            if done[i]:
+                continue
+            a, _ = pols[i].schedule(obs[i])
+            assert (int(a["stage_idx"]), int(a["num_exec"])) == (int(si[i]), int(ne[i])), f"env{i} step{k}"
+        eng.step(si, ne)
+        for i in range(B):
+            if not done[i]:
+                obs[i], _, done[i], _, _ = oracles[i].step({"stage_idx": int(si[i]), "num_exec": int(ne[i])})
+    assert all(done)
+
+
+def case_lockstep_config(make, dataset, env_cfg, cfg_over, B, seed0, pol):
+    cfg = dict(env_cfg, **cfg_over)
+    eng = make(cfg, B, dataset, 100000)
+    oracles = [SparkSchedOracle(cfg, dataset) for _ in range(B)]
+    fac = (lambda i: FairPolicy(cfg["num_executors"])) if pol == "fair" else (lambda i: RandomPolicy(42 + i))
+    parity.run_lockstep(eng, oracles, seeds=[seed0 + i for i in range(B)], policy_factory=fac, check_every=7)
+    parity.compare_traces(eng, oracles)
+    ta, tc, _ = eng.job_times_np()
+    parity.compare_job_times(ta, tc, oracles)
+
+
+def case_rollout_replay(make, dataset, env_cfg, kind, B=64, K=400, stride=4):
+    """ssim_rollout (policy+step fused in one launch) logs its actions; replaying them on the oracle
+    reproduces the trace, job times, decision counts and final observation bit-exactly."""
+    eng = make(env_cfg, B, dataset, 8000)
+    seeds = [5000 + i for i in range(B)]
+    eng.reset(seeds=seeds)
+    log = eng.alloc_action_log(K)
+    eng.rollout(kind, 99, K, log)
+    log = np.asarray(eng.to_numpy(log))
+    v = eng.host_views()
+    ta, tc, _ = eng.job_times_np()
+    for i in range(0, B, stride):
+        o = SparkSchedOracle(env_cfg, dataset)
+        o.trace = []
+        ob, _ = o.reset(seed=seeds[i])
+        c = v["counts"][i]
+        for k in range(int(c[_abi.OC_DECISIONS])):
+            ob, rew, term, _, info = o.step({"stage_idx": int(log[k, i, 0]), "num_exec": int(log[k, i, 1])})
+        assert int(c[_abi.OC_ERR]) == 0
+        assert bool(c[_abi.OC_TERMINATED]) == o.terminated
+        assert float(v["wall_time"][i]) == float(o.wall_time)
+        parity.compare_obs(ob, obs_dict(v, i), f"env{i} final")
+        got = decode_trace(np.asarray(v["trace"][i]), int(c[_abi.OC_TRACE_LEN]))
+        ref = [tuple(float(x) if j == 0 else int(x) for j, x in enumerate(r)) for r in o.trace]
+        assert len(ref) == int(c[_abi.OC_TRACE_LEN]) and got == ref[: len(got)]
+        for jid, job in o.jobs.items():
+            assert ta[i][jid] == job.t_arrival
+            assert tc[i][jid] == job.t_completed or (np.isinf(tc[i][jid]) and np.isinf(job.t_completed))
+
+
+def case_invalid_actions(make, dataset, env_cfg, B=8):
+    """ValueError/KeyError cases of _take_action (spark_sched_sim.py:276-295) -> per-env error bits, state
+    untouched; a following valid action proceeds exactly like the oracle."""
+    N = env_cfg["num_executors"]
+    eng = make(env_cfg, B, dataset, 0)
+    oracles = [SparkSchedOracle(env_cfg, dataset) for _ in range(B)]
+    obs = [o.reset(seed=3 + i)[0] for i, o in enumerate(oracles)]
+    eng.reset(seeds=[3 + i for i in range(B)])
+    pols = [FairPolicy(N) for _ in range(B)]
+    for _ in range(37):  # move into mid-episode states (some with 0 < committable < N)
+        acts = [pols[i].schedule(obs[i])[0] for i in range(B)]
+        eng.step([a["stage_idx"] for a in acts], [a["num_exec"] for a in acts])
+        obs = [oracles[i].step(acts[i])[0] for i in range(B)]
+    v = eng.host_views()
+    bad, expect = [], []
+    for i in range(B):
+        c = v["counts"][i]
+        nn, ns, cm = int(c[_abi.OC_NUM_NODES]), int(c[_abi.OC_NUM_SCHEDULABLE]), int(c[_abi.OC_COMMITTABLE])
+        kind = i % 4
+        if kind == 0:
+            bad.append((nn, 1)), expect.append(_abi.SSIM_ERR_SPACE)
+        elif kind == 1:
+            bad.append((-1, 0)), expect.append(_abi.SSIM_ERR_SPACE)
+        elif kind == 2 and ns < nn:
+            bad.append((ns, 1)), expect.append(_abi.SSIM_ERR_KEY)
+        elif kind == 3 and cm < N:
+            bad.append((0, cm + 1)), expect.append(_abi.SSIM_ERR_TOO_MANY)
+        else:
+            bad.append((0, N + 1)), expect.append(_abi.SSIM_ERR_SPACE)
+    before = eng.snapshot_obs()
+    dec_before = [int(v["counts"][i][_abi.OC_DECISIONS]) for i in range(B)]
+    eng.step([b[0] for b in bad], [b[1] for b in bad])
+    v = eng.host_views()
+    for i in range(B):
+        assert int(v["counts"][i][_abi.OC_ERR]) == expect[i], f"env{i} {bad[i]}"
+        assert int(v["counts"][i][_abi.OC_DECISIONS]) == dec_before[i]
+    for i in range(B):  # the oracle raises on the same actions
+        with pytest.raises((ValueError, KeyError)):
+            oracles[i].step({"stage_idx": bad[i][0], "num_exec": bad[i][1]})
+    after = eng.snapshot_obs()
+    L = eng.layout
+    lo, hi = L.ob_counts, L.ob_counts + L.num_envs * _abi.NUM_COUNTS * 4
+    assert np.array_equal(before[:lo], after[:lo]) and np.array_equal(before[hi:], after[hi:])
+    acts = [pols[i].schedule(obs[i])[0] for i in range(B)]
+    eng.step([a["stage_idx"] for a in acts], [a["num_exec"] for a in acts])
+    v = eng.host_views()
+    for i in range(B):
+        ob, rew, term, _, info = oracles[i].step(acts[i])
+        parity.compare_obs(ob, obs_dict(v, i), f"env{i}")
+        assert int(v["counts"][i][_abi.OC_ERR]) == 0
+
+
+def case_reset_continuation(make, dataset, env_cfg, B=3):
+    """reset(seed=None) continues each env's Generator where the device left it (gymnasium semantics)."""
+    eng = make(env_cfg, B, dataset, 0)
+    oracles = [SparkSchedOracle(env_cfg, dataset) for _ in range(B)]
+    parity.run_lockstep(eng, oracles, seeds=[900 + i for i in range(B)], max_steps=150)
+    obs = [o.reset(seed=None)[0] for o in oracles]
+    eng.reset(seeds=None)
+    v = eng.host_views()
+    for i in range(B):
+        parity.compare_obs(obs[i], obs_dict(v, i), f"env{i} reset(None)")
+        assert int(v["counts"][i][_abi.OC_EPISODE]) == 2
+    pols = [FairPolicy(env_cfg["num_executors"]) for _ in range(B)]
+    for k in range(120):
+        acts = [pols[i].schedule(obs[i])[0] for i in range(B)]
+        eng.step([a["stage_idx"] for a in acts], [a["num_exec"] for a in acts])
+        v = eng.host_views()
+        for i in range(B):
+            obs[i], r, t, _, info = oracles[i].step(acts[i])
+            parity.compare_obs(obs[i], obs_dict(v, i), f"env{i} step{k}")
+            assert float(v["wall_time"][i]) == float(info["wall_time"])

@@ -1,0 +1,154 @@
+"""Python driver for the TEST-ONLY host build of the engine (hostsim.cpp). Mirrors DeviceEngine's API with
+numpy arrays over host memory so the same parity harness drives both."""
+
+from __future__ import annotations
+
+import ctypes as ct
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "gym-sparksched_amd"))
+
+from spark_sched_sim import _abi  # noqa: E402
+from spark_sched_sim._abi import SsimConfig, SsimDataset, SsimLayout  # noqa: E402
+from spark_sched_sim.data_samplers.tpch_pack import PackedDataset, pack  # noqa: E402
+from spark_sched_sim.engine import _ResetSampler, arena_views, make_config  # noqa: E402
+
+SO_PATH = os.path.join(HERE, "_hostsim.so")
+SOURCES = [os.path.join(HERE, "hostsim.cpp")] + [
+    os.path.join(REPO, "gym-sparksched_amd", "csrc", f) for f in ("engine.h", "policy.h", "pyset.h", "pcg64.h",
+                                                                  "layout.h")] + [
+    os.path.join(REPO, "include", "sparksched.h")]
+
+_lib = None
+
+
+def build(force: bool = False, extra_flags=()) -> str:
+    newest = max(os.path.getmtime(p) for p in SOURCES)
+    if force or not os.path.exists(SO_PATH) or os.path.getmtime(SO_PATH) < newest:
+        cmd = ["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function",
+               f"-I{os.path.join(REPO, 'include')}", f"-I{os.path.join(REPO, 'gym-sparksched_amd', 'csrc')}",
+               SOURCES[0], "-o", SO_PATH + ".tmp", *extra_flags]
+        subprocess.run(cmd, check=True)
+        os.replace(SO_PATH + ".tmp", SO_PATH)
+    return SO_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = ct.CDLL(build())
+        vp = ct.c_void_p
+        L.hs_create.argtypes = [ct.POINTER(SsimConfig), ct.POINTER(SsimDataset), ct.POINTER(vp),
+                                ct.POINTER(SsimLayout)]
+        L.hs_destroy.argtypes = [vp]
+        for n in ("hs_obs", "hs_reset_arena", "hs_state"):
+            getattr(L, n).argtypes = [vp]
+            getattr(L, n).restype = ct.POINTER(ct.c_uint8)
+        L.hs_reset.argtypes = [vp]
+        L.hs_step.argtypes = [vp, vp, vp]
+        L.hs_policy.argtypes = [vp, ct.c_int, ct.c_uint64, ct.c_uint64, vp, vp]
+        L.hs_rollout.argtypes = [vp, ct.c_int, ct.c_uint64, ct.c_int, vp]
+        L.hs_pcg_run.argtypes = [vp, vp, ct.c_int, vp]
+        L.hs_job_times.argtypes = [vp, vp, vp, vp]
+        L.hs_pyset_trace.argtypes = [vp, ct.c_int, ct.c_int, vp]
+        _lib = L
+    return _lib
+
+
+class HostEngine:
+    def __init__(self, env_cfg: dict, num_envs: int, dataset, job_cap=None, trace_cap: int = 0):
+        N = env_cfg["num_executors"]
+        packed = dataset if isinstance(dataset, PackedDataset) else pack(dataset, N)
+        self.packed = packed.with_executors(N)
+        self.cfg = make_config(env_cfg, num_envs, self.packed, job_cap, trace_cap)
+        self.num_envs = num_envs
+        self._arrays = [np.ascontiguousarray(a) for a in self.packed.arrays()]
+        self.ds = SsimDataset(self.packed.num_templates, self.packed.num_template_stages,
+                              *[a.ctypes.data for a in self._arrays])
+        self.layout = SsimLayout()
+        h = ct.c_void_p()
+        rc = lib().hs_create(ct.byref(self.cfg), ct.byref(self.ds), ct.byref(h), ct.byref(self.layout))
+        assert rc == 0
+        self.handle = h
+        L = self.layout
+        self.obs = np.ctypeslib.as_array(lib().hs_obs(h), shape=(L.obs_bytes,))
+        self.reset_buf = np.ctypeslib.as_array(lib().hs_reset_arena(h), shape=(L.reset_bytes,))
+        self.state = np.ctypeslib.as_array(lib().hs_state(h), shape=(L.state_bytes,))
+        self.views = arena_views(self.obs, L)
+        self.sampler = _ResetSampler(dict(env_cfg), self.cfg.job_cap, num_envs)
+        self.actions = np.zeros((2, num_envs), dtype=np.int32)
+
+    def _rng_words(self, env):
+        off = 4096 + env * self.layout.env_bytes + 16
+        raw = self.state[off: off + 40]
+        w = raw[:32].view(np.uint64)
+        u = raw[32:40].view(np.uint32)
+        return int(w[0]), int(w[1]), int(w[2]), int(w[3]), int(u[0]), int(u[1])
+
+    def reset(self, seeds=None, options=None, env_ids=None):
+        ids = range(self.num_envs) if env_ids is None else list(env_ids)
+        self.reset_buf[:] = 0
+        for k, e in enumerate(ids):
+            if seeds is None:
+                s = None
+            elif np.isscalar(seeds):
+                s = int(seeds) + e
+            else:
+                s = int(seeds[k])
+            opt = options[k] if isinstance(options, (list, tuple)) else options
+            self.sampler.fill(self.reset_buf, self.layout.reset_stride, e, s, opt, self._rng_words)
+        lib().hs_reset(self.handle)
+
+    def step(self, stage_idx, num_exec):
+        si = np.ascontiguousarray(np.asarray(stage_idx, dtype=np.int32).reshape(self.num_envs))
+        ne = np.ascontiguousarray(np.asarray(num_exec, dtype=np.int32).reshape(self.num_envs))
+        lib().hs_step(self.handle, si.ctypes.data, ne.ctypes.data)
+
+    def policy(self, kind, seed=0, counter=0):
+        a = self.actions
+        lib().hs_policy(self.handle, kind, seed, counter, a[0].ctypes.data, a[1].ctypes.data)
+        return a[0].copy(), a[1].copy()
+
+    def rollout(self, kind, seed, num_steps, action_log=None):
+        ptr = action_log.ctypes.data if action_log is not None else None
+        lib().hs_rollout(self.handle, kind, seed, num_steps, ptr)
+
+    def host_views(self):
+        return self.views
+
+    def job_times_np(self):
+        B, J = self.num_envs, self.cfg.job_cap
+        ta, tc = np.zeros((B, J)), np.zeros((B, J))
+        st = np.zeros((B, J), dtype=np.int32)
+        lib().hs_job_times(self.handle, ta.ctypes.data, tc.ctypes.data, st.ctypes.data)
+        return ta, tc, st
+
+    def alloc_action_log(self, num_steps):
+        return np.zeros((num_steps, self.num_envs, 2), dtype=np.int32)
+
+    @staticmethod
+    def to_numpy(x):
+        return x
+
+    def snapshot_obs(self):
+        return self.obs.copy()
+
+    def close(self):
+        if self.handle is not None:
+            lib().hs_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+__all__ = ["HostEngine", "build", "lib", "_abi"]

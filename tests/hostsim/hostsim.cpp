@@ -1,0 +1,220 @@
+// hostsim.cpp — TEST-ONLY host build of the device engine (gym-sparksched_amd/csrc/engine.h, policy.h).
+//
+// Not part of the product: the product is the gfx950 library (sparksched.hip) and nothing in the
+// product loads this file's output. It instantiates the same Sim<W>/PolicyView<W> templates with a
+// one-lane wave (W::kWidth = 1) so the simulation logic can be checked against the CPU oracle, with host
+// sanitizers, in a container that has no GPU. Device parity is checked separately by the `-m gpu` tests.
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "engine.h"
+#include "policy.h"
+
+using namespace ssim;
+
+struct WaveSerial {
+  static constexpr int kWidth = 1;
+  static int lane() { return 0; }
+  static uint64_t ballot(bool p) { return p ? 1u : 0u; }
+  static int ffs(uint64_t m) { return m ? __builtin_ctzll(m) : -1; }
+  static int popc(uint64_t m) { return __builtin_popcountll(m); }
+  static int rank(uint64_t) { return 0; }
+  static int bcast_i(int v, int) { return v; }
+  static void sync() {}
+  static int excl_scan(int x, int* total) {
+    *total = x;
+    return 0;
+  }
+  static double sum_d(double x) { return x; }
+  static void min_pair(int&, int&) {}
+  static void min_event(double&, int&, int&) {}
+};
+
+struct hs_handle {
+  Params* params;
+  uint8_t* state;
+  uint8_t* obs;
+  uint8_t* reset;
+  uint8_t* scratch;
+};
+
+extern "C" {
+
+int hs_create(const ssim_config* cfg, const ssim_dataset* ds, hs_handle** out, ssim_layout* layout_out) {
+  hs_handle* h = (hs_handle*)calloc(1, sizeof(hs_handle));
+  Params p;
+  memset(&p, 0, sizeof(p));
+  if (!compute_layout(*cfg, &p.L, &p.O)) {
+    free(h);
+    return -1;
+  }
+  p.D = *ds;
+  p.C = *cfg;
+  h->state = (uint8_t*)calloc(1, (size_t)p.L.state_bytes);
+  h->obs = (uint8_t*)calloc(1, (size_t)p.L.obs_bytes);
+  h->reset = (uint8_t*)calloc(1, (size_t)p.L.reset_bytes);
+  h->scratch = (uint8_t*)calloc(1, (size_t)p.L.scratch_bytes);
+  memcpy(h->state, &p, sizeof(Params));
+  h->params = (Params*)h->state;
+  *layout_out = p.L;
+  *out = h;
+  return 0;
+}
+
+void hs_destroy(hs_handle* h) {
+  free(h->state);
+  free(h->obs);
+  free(h->reset);
+  free(h->scratch);
+  free(h);
+}
+
+uint8_t* hs_obs(hs_handle* h) { return h->obs; }
+uint8_t* hs_reset_arena(hs_handle* h) { return h->reset; }
+uint8_t* hs_state(hs_handle* h) { return h->state; }
+
+int hs_reset(hs_handle* h) {
+  const Params* P = h->params;
+  for (int e = 0; e < P->L.num_envs; ++e) {
+    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e);
+    s.reset(h->reset + (int64_t)e * P->L.reset_stride);
+  }
+  return 0;
+}
+
+int hs_step(hs_handle* h, const int32_t* stage_idx, const int32_t* num_exec) {
+  const Params* P = h->params;
+  for (int e = 0; e < P->L.num_envs; ++e) {
+    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e);
+    StepIn a;
+    a.stage_idx = stage_idx[e];
+    a.num_exec = num_exec[e];
+    s.step(a);
+  }
+  return 0;
+}
+
+int hs_policy(hs_handle* h, int kind, uint64_t seed, uint64_t counter, int32_t* stage_idx, int32_t* num_exec) {
+  const Params* P = h->params;
+  for (int e = 0; e < P->L.num_envs; ++e) {
+    PolicyView<WaveSerial> v{P->L, h->obs, e};
+    const StepIn a = v.act(kind, seed, counter);
+    stage_idx[e] = a.stage_idx;
+    num_exec[e] = a.num_exec;
+  }
+  return 0;
+}
+
+int hs_rollout(hs_handle* h, int kind, uint64_t seed, int num_steps, int32_t* action_log) {
+  const Params* P = h->params;
+  const int B = P->L.num_envs;
+  for (int e = 0; e < B; ++e) {
+    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e);
+    PolicyView<WaveSerial> v{P->L, h->obs, e};
+    for (int k = 0; k < num_steps; ++k) {
+      const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.env + P->O.hdr);
+      const StepIn a = v.act(kind, seed, (uint64_t)hd->decisions + ((uint64_t)hd->episode << 32));
+      if (action_log) {
+        action_log[((int64_t)k * B + e) * 2 + 0] = a.stage_idx;
+        action_log[((int64_t)k * B + e) * 2 + 1] = a.num_exec;
+      }
+      s.step(a);
+    }
+  }
+  return 0;
+}
+
+void hs_job_times(hs_handle* h, double* ta, double* tc, int32_t* st) {
+  const Params* P = h->params;
+  const int J = P->L.job_cap;
+  for (int e = 0; e < P->L.num_envs; ++e) {
+    const uint8_t* env = h->state + kParamsReserve + (int64_t)e * P->L.env_bytes;
+    memcpy(ta + (int64_t)e * J, env + P->O.job_tarr, 8 * (size_t)J);
+    memcpy(tc + (int64_t)e * J, env + P->O.job_tdone, 8 * (size_t)J);
+    memcpy(st + (int64_t)e * J, env + P->O.job_state, 4 * (size_t)J);
+  }
+}
+
+// PCG64 / CPython-set models exposed for the known-answer tests.
+void hs_pcg_run(uint64_t* words, const int32_t* ops, int n_ops, double* out) {
+  Pcg64 r;
+  r.s_hi = words[0];
+  r.s_lo = words[1];
+  r.i_hi = words[2];
+  r.i_lo = words[3];
+  r.has32 = (uint32_t)words[4];
+  r.u32 = (uint32_t)words[5];
+  for (int k = 0; k < n_ops; ++k) {
+    const int op = ops[k];
+    out[k] = op == 0 ? r.random() : (double)r.bounded((uint32_t)op);
+  }
+  words[0] = r.s_hi;
+  words[1] = r.s_lo;
+  words[2] = r.i_hi;
+  words[3] = r.i_lo;
+  words[4] = r.has32;
+  words[5] = r.u32;
+}
+
+// Runs a trace of set operations; after each op writes the iteration order into `orders`
+// (row of `width` int32, -1 padded). ops: (code, key) pairs; code 0 add, 1 remove, 2 copy,
+// 3 "set(filtered)" with keys whose bit in `key` (bitmask over key%31) is set, 4 pop.
+int hs_pyset_trace(const int32_t* ops, int n_ops, int width, int32_t* orders) {
+  PySetMeta m;
+  uint8_t* tab = (uint8_t*)malloc(4096);
+  uint8_t* tab2 = (uint8_t*)malloc(4096);
+  int32_t keys[1024], tmp[1024];
+  ps_init(&m, tab);
+  uint32_t finger = 0;
+  for (int k = 0; k < n_ops; ++k) {
+    const int code = ops[2 * k], key = ops[2 * k + 1];
+    if (code == 0) {
+      ps_add(&m, tab, (uint32_t)key, tmp);
+    } else if (code == 1) {
+      if (!ps_remove(&m, tab, (uint32_t)key)) return -1;
+    } else if (code == 2) {  // s = s.copy()
+      int n = ps_keys(&m, tab, keys);
+      memcpy(tab2, tab, (size_t)m.mask + 1);
+      PySetMeta src = m;
+      ps_copy_order(&src, keys, n, tab2);
+      // materialise the copy as the current set: clean table with that order
+      uint32_t size = 8;
+      if (n * 5 >= 21)
+        while ((int)size <= n * 2) size <<= 1;
+      if (!((size - 1) == src.mask && src.fill == src.used)) {
+        for (uint32_t i = 0; i < size; ++i) tab[i] = kSlotEmpty;
+        for (int i = 0; i < n; ++i) ps_insert_clean(tab, size - 1, (uint32_t)keys[i]);
+        m.mask = (uint16_t)(size - 1);
+      }
+      m.fill = m.used = (uint16_t)n;
+      finger = 0;
+    } else if (code == 3) {  // s = set(x for x in s if mask bit)
+      int n = ps_keys(&m, tab, keys);
+      int c = 0;
+      for (int i = 0; i < n; ++i)
+        if ((key >> (keys[i] % 31)) & 1) keys[c++] = keys[i];
+      ps_init(&m, tab);
+      for (int i = 0; i < c; ++i) ps_add(&m, tab, (uint32_t)keys[i], tmp);
+      finger = 0;
+    } else if (code == 4) {  // pop
+      if (m.used == 0) return -2;
+      uint32_t i = finger & m.mask;
+      while (tab[i] >= kSlotDummy) i = (i + 1) & m.mask;
+      tab[i] = kSlotDummy;
+      m.used--;
+      finger = i + 1;
+    }
+    int n = ps_keys(&m, tab, keys);
+    if (n > width) return -3;
+    for (int i = 0; i < width; ++i) orders[(int64_t)k * width + i] = i < n ? keys[i] : -1;
+  }
+  free(tab);
+  free(tab2);
+  return 0;
+}
+
+}  // extern "C"

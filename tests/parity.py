@@ -1,0 +1,130 @@
+"""Shared parity harness: drive the CPU oracle and an engine (device or host build) with identical seeds and
+actions, and compare every observation, reward, flag, wall time, the event trace and job completion times.
+
+Comparison rules (north star, BASELINE.json): integers / event order / executor assignments bit-exact;
+float64 wall-clock and job times bit-exact (same IEEE adds); rewards within 1e-9 relative (set-order
+summation in the reference); float32 node features bit-exact.
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "gym-sparksched_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from oracle.policies import FairPolicy  # noqa: E402
+from oracle.restatement import SparkSchedOracle  # noqa: E402
+from spark_sched_sim import _abi  # noqa: E402
+from spark_sched_sim.engine import decode_trace, obs_dict  # noqa: E402
+
+REWARD_RTOL = 1e-9
+
+
+class Mismatch(AssertionError):
+    pass
+
+
+def compare_obs(ref: dict, got: dict, where: str) -> None:
+    rn, gn = ref["dag_batch"].nodes, got["dag_batch"].nodes
+    if rn.shape != gn.shape or not np.array_equal(rn.view(np.uint32), gn.view(np.uint32)):
+        raise Mismatch(f"{where}: nodes differ\nref={rn}\ngot={gn}")
+    re_, ge = ref["dag_batch"].edge_links, got["dag_batch"].edge_links
+    if re_.shape != ge.shape or not np.array_equal(re_, ge):
+        raise Mismatch(f"{where}: edge_links differ\nref={re_.tolist()}\ngot={ge.tolist()}")
+    for k in ("dag_ptr", "num_committable_execs", "source_job_idx", "exec_supplies"):
+        if list(np.atleast_1d(ref[k])) != list(np.atleast_1d(got[k])):
+            raise Mismatch(f"{where}: {k} differ ref={ref[k]} got={got[k]}")
+
+
+def close_rel(a: float, b: float, rtol: float = REWARD_RTOL) -> bool:
+    return a == b or abs(a - b) <= rtol * max(abs(a), abs(b), 1e-300)
+
+
+def run_lockstep(engine, oracles, seeds, policy_factory=None, max_steps=10**9, check_every=1, actions_fn=None):
+    """Drive B oracles and a B-env engine in lockstep.
+
+    actions for each env come from `policy_factory(i)(oracle_obs)` (CPU oracle policy), unless `actions_fn`
+    is given: actions_fn(step) -> (stage_idx[B], num_exec[B]) (e.g. device-policy replay).
+    Returns per-env number of decisions."""
+    B = len(oracles)
+    pols = [policy_factory(i) if policy_factory else FairPolicy(oracles[i].N) for i in range(B)]
+    obs = []
+    for i, o in enumerate(oracles):
+        o.trace = []
+        ob, _ = o.reset(seed=int(seeds[i]))
+        obs.append(ob)
+    engine.reset(seeds=list(map(int, seeds)))
+    v = engine.host_views()
+    for i in range(B):
+        compare_obs(obs[i], obs_dict(v, i), f"env{i} reset")
+    done = [False] * B
+    steps = [0] * B
+    for k in range(max_steps):
+        if all(done):
+            break
+        si = np.full(B, -1, dtype=np.int32)
+        ne = np.ones(B, dtype=np.int32)
+        if actions_fn is not None:
+            si[:], ne[:] = actions_fn(k)
+        for i in range(B):
+            if done[i]:
+                continue
+            if actions_fn is None:
+                a, _ = pols[i].schedule(obs[i])
+                si[i], ne[i] = int(a["stage_idx"]), int(a["num_exec"])
+        engine.step(si, ne)
+        v = engine.host_views()
+        for i in range(B):
+            if done[i]:
+                continue
+            ob, rew, term, _, info = oracles[i].step({"stage_idx": int(si[i]), "num_exec": int(ne[i])})
+            obs[i] = ob
+            steps[i] += 1
+            c = v["counts"][i]
+            if int(c[_abi.OC_ERR]) != 0:
+                raise Mismatch(f"env{i} step{k}: engine error bits {int(c[_abi.OC_ERR]):#x}")
+            got_wall = float(v["wall_time"][i])
+            if got_wall != float(info["wall_time"]):
+                raise Mismatch(f"env{i} step{k}: wall {got_wall!r} != {info['wall_time']!r}")
+            got_r = float(v["reward"][i])
+            if not close_rel(got_r, float(rew)):
+                raise Mismatch(f"env{i} step{k}: reward {got_r!r} != {rew!r}")
+            if bool(c[_abi.OC_TERMINATED]) != bool(term):
+                raise Mismatch(f"env{i} step{k}: terminated {bool(c[_abi.OC_TERMINATED])} != {term}")
+            if k % check_every == 0 or term:
+                compare_obs(ob, obs_dict(v, i), f"env{i} step{k}")
+            if int(c[_abi.OC_DECISIONS]) != oracles[i].decisions:
+                raise Mismatch(f"env{i} step{k}: decisions {int(c[_abi.OC_DECISIONS])} != {oracles[i].decisions}")
+            done[i] = bool(term)
+    return steps
+
+
+def compare_traces(engine, oracles) -> None:
+    v = engine.host_views()
+    for i, o in enumerate(oracles):
+        n = int(v["counts"][i][_abi.OC_TRACE_LEN])
+        got = decode_trace(np.asarray(v["trace"][i]), n)
+        ref = [(float(t), int(kd), int(e), int(j), int(s), int(q)) for (t, kd, e, j, s, q) in o.trace]
+        if n != len(ref) or got != ref[: len(got)]:
+            for idx, (a, b) in enumerate(zip(ref, got)):
+                if a != b:
+                    raise Mismatch(f"env{i}: trace differs at record {idx}: ref={a} got={b} (lens {len(ref)}/{n})")
+            raise Mismatch(f"env{i}: trace length ref={len(ref)} got={n}")
+
+
+def compare_job_times(ta, tc, oracles) -> None:
+    for i, o in enumerate(oracles):
+        for jid, job in o.jobs.items():
+            if float(ta[i][jid]) != float(job.t_arrival):
+                raise Mismatch(f"env{i} job{jid}: t_arrival {ta[i][jid]!r} != {job.t_arrival!r}")
+            ref_c = float(job.t_completed)
+            got_c = float(tc[i][jid])
+            if not (ref_c == got_c or (math.isinf(ref_c) and math.isinf(got_c))):
+                raise Mismatch(f"env{i} job{jid}: t_completed {got_c!r} != {ref_c!r}")

@@ -1,0 +1,55 @@
+"""Device parity (`-m gpu`): the gfx950 kernels through the C ABI vs the CPU oracle (cases.py)."""
+
+import pytest
+
+import cases
+from spark_sched_sim import _abi
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def make(gpu_device):
+    from spark_sched_sim.engine import DeviceEngine
+
+    def _make(cfg, B, ds, trace_cap):
+        return DeviceEngine(cfg, B, ds, device=gpu_device, trace_cap=trace_cap)
+
+    return _make
+
+
+def test_native_library_is_the_hip_build(gpu_device):
+    from spark_sched_sim import native
+
+    L = native.lib()
+    assert native.LIB_PATH.endswith("libsparksched.so") and hasattr(L, "ssim_step")
+
+
+def test_lockstep_fair(make, dataset, env_cfg):
+    cases.case_lockstep_fair(make, dataset, env_cfg)
+
+
+def test_device_fair_policy(make, dataset, env_cfg):
+    cases.case_device_fair_policy(make, dataset, env_cfg)
+
+
+@pytest.mark.parametrize("cfg_over,B,seed0,pol", cases.LOCKSTEP_CONFIGS)
+def test_lockstep_configs(make, dataset, env_cfg, cfg_over, B, seed0, pol):
+    cases.case_lockstep_config(make, dataset, env_cfg, cfg_over, B, seed0, pol)
+
+
+@pytest.mark.parametrize("kind", [_abi.SSIM_POLICY_RANDOM, _abi.SSIM_POLICY_FAIR])
+def test_rollout_replay(make, dataset, env_cfg, kind):
+    cases.case_rollout_replay(make, dataset, env_cfg, kind)
+
+
+def test_rollout_replay_full_episodes(make, dataset, env_cfg):
+    cases.case_rollout_replay(make, dataset, env_cfg, _abi.SSIM_POLICY_RANDOM, B=256, K=2500, stride=32)
+
+
+def test_invalid_actions(make, dataset, env_cfg):
+    cases.case_invalid_actions(make, dataset, env_cfg)
+
+
+def test_reset_continuation(make, dataset, env_cfg):
+    cases.case_reset_continuation(make, dataset, env_cfg)
