@@ -1,0 +1,30 @@
+#!/bin/bash
+# GPU-box check runner: each step has its own time limit; a fault-like exit (timeout 124/137,
+# abort 134, segfault 139, >128) stops the script before any further GPU work. Ordinary failures
+# (exit 1, e.g. a failing test) are recorded and the next step runs.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+step() {
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name: fault-like exit $rc"; exit $rc; fi
+}
+for s in "$@"; do
+  case "$s" in
+    smoke)   step smoke 300 python __graft_entry__.py ;;
+    pytest)  step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    bench)   step bench 400 python bench.py ;;
+    bench_nocpu) step bench_nocpu 300 python bench.py --no-cpu-baseline ;;
+    bench_step) step bench_step 300 python bench.py --no-cpu-baseline --mode step ;;
+    prof)    step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
+    prof_step) step prof_step 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_step" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "=== done"

@@ -1,0 +1,105 @@
+"""Generates the committed golden fixtures in tests/golden/ from the CPU oracle (oracle/restatement.py).
+
+The reference itself cannot be run here and its test suite holds no vectors,
+so these fixtures pin (a) the oracle against regressions and (b) every engine build against the oracle.
+Each fixture records, per decision of a full episode, a digest of the observation plus the scalars, the
+full event trace digest and the job completion times. Usage: python tests/golden/make_golden.py
+"""
+
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+for p in (REPO, os.path.join(REPO, "gym-sparksched_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from oracle.policies import FairPolicy, RandomPolicy  # noqa: E402
+from oracle.restatement import SparkSchedOracle  # noqa: E402
+from spark_sched_sim.data_samplers.synthetic_tpch import generate  # noqa: E402
+from spark_sched_sim.data_samplers.tpch_pack import pack  # noqa: E402
+
+FIXTURES = {
+    # examples.py:84 run_episode(seed=1234) with the fair scheduler, examples.py:15-23 config
+    "fair_j50_n10_seed1234": dict(cfg=dict(num_executors=10, job_arrival_cap=50, job_arrival_rate=4.0e-5,
+                                           moving_delay=2000.0, warmup_delay=1000.0), seed=1234, policy="fair"),
+    # small case (J=5, N=4), reference RandomScheduler(seed=42)
+    "random_j5_n4_seed7": dict(cfg=dict(num_executors=4, job_arrival_cap=5, job_arrival_rate=4.0e-5,
+                                        moving_delay=2000.0, warmup_delay=1000.0), seed=7, policy="random"),
+    # discounted reward (trainer.py:72-74 beta), decima_tpch.yaml env section scaled to 20 jobs
+    "random_j20_n50_beta_seed11": dict(cfg=dict(num_executors=50, job_arrival_cap=20, job_arrival_rate=4.0e-5,
+                                                moving_delay=2000.0, warmup_delay=1000.0, beta=5e-3), seed=11,
+                                       policy="random"),
+}
+
+
+def obs_digest(obs) -> str:
+    h = hashlib.sha1()
+    g = obs["dag_batch"]
+    h.update(np.ascontiguousarray(g.nodes, dtype=np.float32).tobytes())
+    h.update(np.ascontiguousarray(g.edge_links, dtype=np.int64).tobytes())
+    h.update(np.asarray(obs["dag_ptr"], dtype=np.int64).tobytes())
+    h.update(np.asarray(obs["exec_supplies"], dtype=np.int64).tobytes())
+    h.update(np.asarray([obs["num_committable_execs"], obs["source_job_idx"]], dtype=np.int64).tobytes())
+    return h.hexdigest()[:20]
+
+
+def trace_digest(trace) -> str:
+    h = hashlib.sha256()
+    for t, kind, e, j, s, q in trace:
+        h.update(np.float64(t).tobytes() + np.asarray([kind, e, j, s, q], dtype=np.int64).tobytes())
+    return h.hexdigest()
+
+
+def dataset_digest(ds) -> str:
+    h = hashlib.sha256()
+    for a in pack(ds, 10).arrays():
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def record(name: str, spec: dict, ds) -> dict:
+    env = SparkSchedOracle(spec["cfg"], ds)
+    env.trace = []
+    pol = FairPolicy(spec["cfg"]["num_executors"]) if spec["policy"] == "fair" else RandomPolicy(42)
+    obs, _ = env.reset(seed=spec["seed"])
+    steps = [{"digest": obs_digest(obs), "reward": 0.0, "wall": 0.0}]
+    actions = []
+    done = False
+    while not done:
+        a, _ = pol.schedule(obs)
+        act = (int(a["stage_idx"]), int(a["num_exec"]))
+        actions.append(act)
+        obs, r, done, _, info = env.step({"stage_idx": act[0], "num_exec": act[1]})
+        steps.append({"digest": obs_digest(obs), "reward": float(r), "wall": float(info["wall_time"]),
+                      "nodes": int(obs["dag_batch"].nodes.shape[0]), "edges": int(len(obs["dag_batch"].edge_links)),
+                      "committable": int(obs["num_committable_execs"])})
+    return {
+        "name": name, "cfg": spec["cfg"], "seed": spec["seed"], "policy": spec["policy"],
+        "dataset_seed": 0, "dataset_sha256": dataset_digest(ds),
+        "decisions": len(actions), "actions": actions, "steps": steps,
+        "trace_len": len(env.trace), "trace_sha256": trace_digest(env.trace),
+        "job_t_arrival": [float(env.jobs[j].t_arrival) for j in sorted(env.jobs)],
+        "job_t_completed": [float(env.jobs[j].t_completed) for j in sorted(env.jobs)],
+        "avg_job_duration_s": float(np.mean(env.duration_buff)) * 1e-3,
+    }
+
+
+def main():
+    ds = generate(0)
+    for name, spec in FIXTURES.items():
+        fx = record(name, spec, ds)
+        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+            json.dump(fx, f, separators=(",", ":"))
+        print(name, fx["decisions"], "decisions", fx["trace_len"], "trace records")
+
+
+if __name__ == "__main__":
+    main()

@@ -181,14 +181,16 @@ int hs_pyset_trace(const int32_t* ops, int n_ops, int width, int32_t* orders) {
       memcpy(tab2, tab, (size_t)m.mask + 1);
       PySetMeta src = m;
       ps_copy_order(&src, keys, n, tab2);
-      // materialise the copy as the current set: clean table with that order
+      // materialise the copy as the current set (ps_copy_order left the copy's table in tab2 unless
+      // it was a slot-for-slot copy of the source table)
       uint32_t size = 8;
       if (n * 5 >= 21)
         while ((int)size <= n * 2) size <<= 1;
-      if (!((size - 1) == src.mask && src.fill == src.used)) {
-        for (uint32_t i = 0; i < size; ++i) tab[i] = kSlotEmpty;
-        for (int i = 0; i < n; ++i) ps_insert_clean(tab, size - 1, (uint32_t)keys[i]);
+      if (n > 0 && !((size - 1) == src.mask && src.fill == src.used)) {
+        memcpy(tab, tab2, size);
         m.mask = (uint16_t)(size - 1);
+      } else if (n == 0) {
+        ps_init(&m, tab);
       }
       m.fill = m.used = (uint16_t)n;
       finger = 0;
