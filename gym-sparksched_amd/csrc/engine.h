@@ -19,8 +19,19 @@
 #include "pcg64.h"
 #include "pyset.h"
 
+// Diagnostic build only (-DSSIM_PROFILE, scripts/phase_profile.py): per-phase shader-clock sums per wave.
+#ifdef SSIM_PROFILE
+#define SSIM_TIC(v) const uint64_t v = W::clock()
+#define SSIM_TOC(v, ph) prof[ph] += W::clock() - (v)
+#else
+#define SSIM_TIC(v) (void)0
+#define SSIM_TOC(v, ph) (void)0
+#endif
+
 namespace ssim {
 
+enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kPhHandle, kPhPostScan, kPhObserve,
+                 kNumPhases };
 enum : int32_t { kPoolNone = -1, kPoolCommon = 0 };
 enum : int32_t { kEvArrival = 1, kEvTask = 2, kEvReady = 3, kTrJobDone = 4 };
 enum : int32_t { kJobPending = 0, kJobActive = 1, kJobDone = 2 };
@@ -53,6 +64,9 @@ struct Sim {
   int32_t eid;   // env index
   EnvHeader h;   // register copy of the header
   Pcg64 rng;
+#ifdef SSIM_PROFILE
+  uint64_t prof[kNumPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
   __device__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* scratch, uint8_t* obs_arena,
                  int32_t env_index)
@@ -732,13 +746,18 @@ struct Sim {
     return true;
   }
 
-  __device__ void simulate() {  // _resume_simulation :320-343
+  // Returns true when it stopped at a decision point (committable executors and a schedulable stage).
+  __device__ bool simulate() {  // _resume_simulation :320-343
     h.step_events = 0;
     for (;;) {
-      if (frozen()) return;
+      if (frozen()) return false;
       double t;
       int kind, e, g, seq;
-      if (!pop_event(&t, &kind, &e, &g, &seq)) return;
+      SSIM_TIC(t_pop);
+      const bool have = pop_event(&t, &kind, &e, &g, &seq);
+      SSIM_TOC(t_pop, kPhPop);
+      if (!have) return false;
+      SSIM_TIC(t_h);
       h.wall = t;
       h.events++;
       h.step_events++;
@@ -753,10 +772,19 @@ struct Sim {
         else
           on_task_done(e, g);
       }
-      if (committable() == 0) continue;
-      if (any_schedulable()) return;
-      release_idle_all(kPoolNone);
-      h.source = kPoolNone;
+      SSIM_TOC(t_h, kPhHandle);
+      SSIM_TIC(t_s);
+      if (committable() == 0) {
+        SSIM_TOC(t_s, kPhPostScan);
+        continue;
+      }
+      const bool found = any_schedulable();
+      if (!found) {
+        release_idle_all(kPoolNone);
+        h.source = kPoolNone;
+      }
+      SSIM_TOC(t_s, kPhPostScan);
+      if (found) return true;
     }
   }
 
@@ -921,6 +949,7 @@ struct Sim {
   __device__ void step(StepIn a) {
     load_header();
     if (h.terminated || frozen() || h.num_jobs == 0) return;
+    SSIM_TIC(t_act);
     const int idx = a.stage_idx, nx = a.num_exec;
     // Discrete(n, start=-1) holds -1 .. n-2; Discrete(N, start=1) holds 1 .. N
     if (idx < -1 || idx > h.stage_idx_n - 2 || nx < 1 || nx > L.num_executors) {
@@ -950,13 +979,21 @@ struct Sim {
     }
     h.decisions++;
     h.step_events = 0;
-    if (committable() > 0 && any_schedulable()) {
+    SSIM_TOC(t_act, kPhAction);
+    SSIM_TIC(t_rc);
+    const bool round_continues = committable() > 0 && any_schedulable();
+    SSIM_TOC(t_rc, kPhRoundCheck);
+    if (round_continues) {
+      SSIM_TIC(t_o);
       observe(0.0);
+      SSIM_TOC(t_o, kPhObserve);
       store_header();
       return;
     }
+    SSIM_TIC(t_f);
     commit_leftovers();
     fulfill_from_source();
+    SSIM_TOC(t_f, kPhFulfill);
     h.source = kPoolNone;
     {  // selected_stages.clear()
       const int32_t* sl = F<int32_t>(O.sel_list);
@@ -968,11 +1005,15 @@ struct Sim {
       W::sync();
     }
     const double t0 = h.wall;
-    simulate();
+    const bool at_decision = simulate();
     const double reward = -jobtime(t0, h.decisions);
     h.terminated = (h.n_completed == h.num_jobs) ? 1 : 0;
-    if (!h.terminated) check(committable() > 0 && any_schedulable());
+    // step's `assert committable and schedulable_stages` (:212-215): simulate() stopped at a decision
+    // point (state untouched since) unless the queue ran dry
+    if (!h.terminated) check(at_decision);
+    SSIM_TIC(t_o);
     observe(reward);
+    SSIM_TOC(t_o, kPhObserve);
     store_header();
   }
 

@@ -33,6 +33,7 @@ struct WaveHip {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
+  __device__ static __forceinline__ uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
   __device__ static __forceinline__ int excl_scan(int x, int* total) {
     int v = x;
     const int l = lane();
@@ -109,14 +110,21 @@ __global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, con
 }
 
 __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
-                                                int kind, uint64_t seed, int num_steps, int32_t* action_log) {
+                                                int kind, uint64_t seed, int num_steps, int32_t* action_log,
+                                                uint64_t* prof_out) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
   Sim<WaveHip> s(P, state, g_smem, obs, eid);
   PolicyView<WaveHip> v{P->L, obs, eid};
   for (int k = 0; k < num_steps; ++k) {
     const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.env + P->O.hdr);
+#ifdef SSIM_PROFILE
+    const uint64_t t0 = WaveHip::clock();
+#endif
     const StepIn a = v.act(kind, seed, (uint64_t)hd->decisions + ((uint64_t)hd->episode << 32));
+#ifdef SSIM_PROFILE
+    s.prof[kPhPolicy] += WaveHip::clock() - t0;
+#endif
     if (action_log != nullptr && WaveHip::lane() == 0) {
       action_log[((int64_t)k * B + eid) * 2 + 0] = a.stage_idx;
       action_log[((int64_t)k * B + eid) * 2 + 1] = a.num_exec;
@@ -124,6 +132,12 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
     WaveHip::sync();
     s.step(a);
   }
+#ifdef SSIM_PROFILE
+  if (prof_out != nullptr && WaveHip::lane() == 0)
+    for (int p = 0; p < kNumPhases; ++p) prof_out[(int64_t)eid * kNumPhases + p] = s.prof[p];
+#else
+  (void)prof_out;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------ C ABI
@@ -232,9 +246,20 @@ extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t
     return set_err(SSIM_E_ARG, "ssim_rollout: unknown policy %d", kind);
   const ssim_layout& L = h->params.L;
   hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
-                     dparams(h), h->state, h->obs, kind, seed, num_steps, action_log);
+                     dparams(h), h->state, h->obs, kind, seed, num_steps, action_log, (uint64_t*)nullptr);
   return hip_check(hipGetLastError(), "k_rollout launch");
 }
+
+#ifdef SSIM_PROFILE
+// Diagnostic build only: same rollout, per-wave phase cycle sums -> prof_out[num_envs][kNumPhases].
+extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
+                                     uint64_t* prof_out, void* stream) {
+  const ssim_layout& L = h->params.L;
+  hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
+                     dparams(h), h->state, h->obs, kind, seed, num_steps, (int32_t*)nullptr, prof_out);
+  return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
+}
+#endif
 
 extern "C" int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32_t* state, void* stream) {
   if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_job_times: null handle");

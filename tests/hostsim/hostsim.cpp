@@ -25,6 +25,7 @@ struct WaveSerial {
   static int rank(uint64_t) { return 0; }
   static int bcast_i(int v, int) { return v; }
   static void sync() {}
+  static uint64_t clock() { return 0; }
   static int excl_scan(int x, int* total) {
     *total = x;
     return 0;
