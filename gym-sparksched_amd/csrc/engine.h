@@ -8,10 +8,14 @@
 // part of the algorithm with identical values, so branches never diverge and same-address loads are
 // broadcast. Data-parallel parts run across lanes through the W policy: the schedulable-stage scan
 // (ballot + first-set-lane), executor event-slot argmin (min-reduce), observation rows and edges
-// (ballot/prefix compaction, coalesced stores), pool-table iteration. W is WaveHip on device
+// (ballot/prefix compaction, coalesced stores), pool-table staging. W is WaveHip on device
 // (sparksched.hip); the test-only host build (tests/hostsim/) instantiates the same template with a
-// one-lane W to debug the logic on CPU. Everything stays in the device's memory spaces: state in HBM
-// (env-major SoA), per-launch scratch in LDS.
+// one-lane W to debug the logic on CPU.
+//
+// Memory. The serial event loop is latency bound, so the env's hot block (header, jobs, compact stage
+// counters, executors, commitments, pool metadata) is copied into LDS for the launch when it fits
+// (`lds_resident`), and CPython-set tables are staged through LDS one pool at a time; HBM sees bulk
+// coalesced copies, the obs stores and the read-only dataset gathers.
 #pragma once
 #include <stdint.h>
 
@@ -58,33 +62,53 @@ struct Sim {
   const StateOffsets& O;
   const ssim_dataset& D;
   const ssim_config& C;
-  uint8_t* env;  // this env's state block
-  uint8_t* scr;  // this env's scratch block
-  uint8_t* obs;  // obs arena base
-  int32_t eid;   // env index
-  EnvHeader h;   // register copy of the header
+  uint8_t* ghot;  // this env's hot block in HBM
+  uint8_t* hot;   // working copy of the hot block (LDS when resident, else == ghot)
+  uint8_t* cold;  // this env's cold block in HBM
+  uint8_t* scr;   // this env's scratch block (LDS)
+  uint8_t* obs;   // obs arena base
+  int32_t eid;    // env index
+  EnvHeader h;    // register copy of the header
   Pcg64 rng;
 #ifdef SSIM_PROFILE
   uint64_t prof[kNumPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 
-  __device__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* scratch, uint8_t* obs_arena,
-                 int32_t env_index)
+  // `lds` = this wave's LDS block: [scratch | hot copy (if resident)]; resident=false keeps hot in HBM.
+  __device__ __forceinline__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* lds,
+                                 uint8_t* obs_arena, int32_t env_index, bool resident)
       : L(p->L), O(p->O), D(p->D), C(p->C),
-        env(state_arena + kParamsReserve + (int64_t)env_index * p->L.env_bytes), scr(scratch),
+        ghot(state_arena + kParamsReserve + (int64_t)env_index * p->L.env_bytes),
+        hot(resident ? lds + p->L.scratch_bytes : state_arena + kParamsReserve + (int64_t)env_index * p->L.env_bytes),
+        cold(state_arena + kParamsReserve + (int64_t)env_index * p->L.env_bytes + p->O.hot_bytes), scr(lds),
         obs(obs_arena), eid(env_index) {}
+
+  // ---------------------------------------------------------------- hot-block residency
+  __device__ __forceinline__ void copy16(uint8_t* dst, const uint8_t* src, int64_t bytes) {
+    W::sync();
+    const int64_t n = bytes >> 4;
+    for (int64_t i = W::lane(); i < n; i += W::kWidth)
+      reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    W::sync();
+  }
+  __device__ __forceinline__ void load_hot() {
+    if (hot != ghot) copy16(hot, ghot, O.hot_bytes);
+  }
+  __device__ __forceinline__ void save_hot() {
+    if (hot != ghot) copy16(ghot, hot, O.hot_bytes);
+  }
 
   // ---------------------------------------------------------------- field access
   template <class T>
-  __device__ __forceinline__ T* F(int64_t off) const {
-    return reinterpret_cast<T*>(env + off);
+  __device__ __forceinline__ T* H(int64_t off) const {
+    return reinterpret_cast<T*>(hot + off);
   }
   template <class T>
   __device__ __forceinline__ T* S(int64_t off) const {
     return reinterpret_cast<T*>(scr + off);
   }
   __device__ __forceinline__ void load_header() {
-    h = *F<EnvHeader>(O.hdr);
+    h = *H<EnvHeader>(O.hdr);
     rng.s_hi = h.rng_s_hi;
     rng.s_lo = h.rng_s_lo;
     rng.i_hi = h.rng_i_hi;
@@ -100,7 +124,7 @@ struct Sim {
     h.rng_has32 = rng.has32;
     h.rng_u32 = rng.u32;
     W::sync();
-    if (W::lane() == 0) *F<EnvHeader>(O.hdr) = h;
+    if (W::lane() == 0) *H<EnvHeader>(O.hdr) = h;
     W::sync();
   }
   __device__ __forceinline__ void fail(uint32_t bits) { h.err |= bits; }
@@ -109,41 +133,39 @@ struct Sim {
     if (!ok) h.err |= SSIM_ERR_INVARIANT;
   }
 
-  // stages (env-global index g = job_base[j] + local stage id)
-  __device__ __forceinline__ int32_t& st_job(int g) const { return F<int32_t>(O.st_job)[g]; }
-  __device__ __forceinline__ int32_t& st_ts(int g) const { return F<int32_t>(O.st_ts)[g]; }
-  __device__ __forceinline__ int32_t& st_rem(int g) const { return F<int32_t>(O.st_rem)[g]; }
-  __device__ __forceinline__ int32_t& st_exe(int g) const { return F<int32_t>(O.st_exe)[g]; }
-  __device__ __forceinline__ int32_t& st_done(int g) const { return F<int32_t>(O.st_done)[g]; }
-  __device__ __forceinline__ int32_t& st_mov(int g) const { return F<int32_t>(O.st_mov)[g]; }
-  __device__ __forceinline__ int32_t& st_com(int g) const { return F<int32_t>(O.st_com)[g]; }
-  __device__ __forceinline__ int32_t& st_unmet(int g) const { return F<int32_t>(O.st_unmet)[g]; }
-  __device__ __forceinline__ int32_t& st_sel(int g) const { return F<int32_t>(O.st_sel)[g]; }
-  __device__ __forceinline__ double& st_recent(int g) const { return F<double>(O.st_recent)[g]; }
-  __device__ __forceinline__ int32_t ntasks(int g) const { return D.ts_num_tasks[st_ts(g)]; }
-  __device__ __forceinline__ bool st_completed(int g) const { return st_done(g) == ntasks(g); }
+  // stages (env-global index g = job_base[j] + local stage id); `done` is derived: rem + exe + done = tasks
+  __device__ __forceinline__ int16_t& st_job(int g) const { return H<int16_t>(O.st_job)[g]; }
+  __device__ __forceinline__ int16_t& st_ts(int g) const { return H<int16_t>(O.st_ts)[g]; }
+  __device__ __forceinline__ int16_t& st_rem(int g) const { return H<int16_t>(O.st_rem)[g]; }
+  __device__ __forceinline__ int16_t& st_exe(int g) const { return H<int16_t>(O.st_exe)[g]; }
+  __device__ __forceinline__ int16_t& st_mov(int g) const { return H<int16_t>(O.st_mov)[g]; }
+  __device__ __forceinline__ int16_t& st_com(int g) const { return H<int16_t>(O.st_com)[g]; }
+  __device__ __forceinline__ int16_t& st_unmet(int g) const { return H<int16_t>(O.st_unmet)[g]; }
+  __device__ __forceinline__ uint8_t& st_sel(int g) const { return H<uint8_t>(O.st_sel)[g]; }
+  __device__ __forceinline__ double& st_recent(int g) const { return reinterpret_cast<double*>(cold + O.st_recent)[g]; }
+  __device__ __forceinline__ bool st_completed(int g) const { return st_rem(g) == 0 && st_exe(g) == 0; }
   // jobs
-  __device__ __forceinline__ int32_t& job_tpl(int j) const { return F<int32_t>(O.job_tpl)[j]; }
-  __device__ __forceinline__ int32_t& job_base(int j) const { return F<int32_t>(O.job_base)[j]; }
-  __device__ __forceinline__ int32_t& job_nst(int j) const { return F<int32_t>(O.job_nst)[j]; }
-  __device__ __forceinline__ int32_t& job_nact(int j) const { return F<int32_t>(O.job_nact)[j]; }
-  __device__ __forceinline__ int32_t& job_sat(int j) const { return F<int32_t>(O.job_sat)[j]; }
-  __device__ __forceinline__ int32_t& job_local(int j) const { return F<int32_t>(O.job_local)[j]; }
-  __device__ __forceinline__ int32_t& job_supply(int j) const { return F<int32_t>(O.job_supply)[j]; }
-  __device__ __forceinline__ int32_t& job_state(int j) const { return F<int32_t>(O.job_state)[j]; }
-  __device__ __forceinline__ int32_t& job_arr_dec(int j) const { return F<int32_t>(O.job_arr_dec)[j]; }
-  __device__ __forceinline__ int32_t& job_done_dec(int j) const { return F<int32_t>(O.job_done_dec)[j]; }
-  __device__ __forceinline__ double& job_tarr(int j) const { return F<double>(O.job_tarr)[j]; }
-  __device__ __forceinline__ double& job_tdone(int j) const { return F<double>(O.job_tdone)[j]; }
+  __device__ __forceinline__ int16_t& job_tpl(int j) const { return H<int16_t>(O.job_tpl)[j]; }
+  __device__ __forceinline__ int16_t& job_base(int j) const { return H<int16_t>(O.job_base)[j]; }
+  __device__ __forceinline__ int16_t& job_nst(int j) const { return H<int16_t>(O.job_nst)[j]; }
+  __device__ __forceinline__ int16_t& job_nact(int j) const { return H<int16_t>(O.job_nact)[j]; }
+  __device__ __forceinline__ int16_t& job_sat(int j) const { return H<int16_t>(O.job_sat)[j]; }
+  __device__ __forceinline__ int16_t& job_local(int j) const { return H<int16_t>(O.job_local)[j]; }
+  __device__ __forceinline__ int16_t& job_supply(int j) const { return H<int16_t>(O.job_supply)[j]; }
+  __device__ __forceinline__ int16_t& job_state(int j) const { return H<int16_t>(O.job_state)[j]; }
+  __device__ __forceinline__ int32_t& job_arr_dec(int j) const { return H<int32_t>(O.job_arr_dec)[j]; }
+  __device__ __forceinline__ int32_t& job_done_dec(int j) const { return H<int32_t>(O.job_done_dec)[j]; }
+  __device__ __forceinline__ double& job_tarr(int j) const { return H<double>(O.job_tarr)[j]; }
+  __device__ __forceinline__ double& job_tdone(int j) const { return H<double>(O.job_tdone)[j]; }
   // executors
-  __device__ __forceinline__ int32_t& ex_loc(int e) const { return F<int32_t>(O.ex_loc)[e]; }
-  __device__ __forceinline__ int32_t& ex_job(int e) const { return F<int32_t>(O.ex_job)[e]; }
-  __device__ __forceinline__ int32_t& ex_task(int e) const { return F<int32_t>(O.ex_task)[e]; }
-  __device__ __forceinline__ int32_t& ex_busy(int e) const { return F<int32_t>(O.ex_busy)[e]; }
-  __device__ __forceinline__ double& ev_t(int e) const { return F<double>(O.ev_t)[e]; }
-  __device__ __forceinline__ int32_t& ev_seq(int e) const { return F<int32_t>(O.ev_seq)[e]; }
-  __device__ __forceinline__ int32_t& ev_type(int e) const { return F<int32_t>(O.ev_type)[e]; }
-  __device__ __forceinline__ int32_t& ev_stage(int e) const { return F<int32_t>(O.ev_stage)[e]; }
+  __device__ __forceinline__ int16_t& ex_loc(int e) const { return H<int16_t>(O.ex_loc)[e]; }
+  __device__ __forceinline__ int16_t& ex_job(int e) const { return H<int16_t>(O.ex_job)[e]; }
+  __device__ __forceinline__ int16_t& ex_task(int e) const { return H<int16_t>(O.ex_task)[e]; }
+  __device__ __forceinline__ int16_t& ex_busy(int e) const { return H<int16_t>(O.ex_busy)[e]; }
+  __device__ __forceinline__ double& ev_t(int e) const { return H<double>(O.ev_t)[e]; }
+  __device__ __forceinline__ int32_t& ev_seq(int e) const { return H<int32_t>(O.ev_seq)[e]; }
+  __device__ __forceinline__ int16_t& ev_type(int e) const { return H<int16_t>(O.ev_type)[e]; }
+  __device__ __forceinline__ int16_t& ev_stage(int e) const { return H<int16_t>(O.ev_stage)[e]; }
   // pools: code 0 = COMMON, 1+j = job j, 1+job_cap+g = stage g, -1 = None
   __device__ __forceinline__ int32_t job_pool(int j) const { return 1 + j; }
   __device__ __forceinline__ int32_t stage_pool(int g) const { return 1 + L.job_cap + g; }
@@ -154,38 +176,38 @@ struct Sim {
     if (p <= L.job_cap) return p - 1;
     return st_job(p - 1 - L.job_cap);
   }
-  __device__ __forceinline__ PySetMeta* pmeta(int p) const { return F<PySetMeta>(O.pool_meta) + p; }
-  __device__ __forceinline__ uint8_t* ptab(int p) const { return F<uint8_t>(O.pool_tab) + (int64_t)p * L.set_cap; }
-  __device__ __forceinline__ int32_t& cfrom(int p) const { return F<int32_t>(O.pool_cfrom)[p]; }
+  __device__ __forceinline__ PySetMeta* pmeta(int p) const { return H<PySetMeta>(O.pool_meta) + p; }
+  __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + O.pool_tab + (int64_t)p * L.set_cap; }
+  __device__ __forceinline__ int16_t& cfrom(int p) const { return H<int16_t>(O.pool_cfrom)[p]; }
   __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)pmeta(p)->used; }
 
   // ---------------------------------------------------------------- tracker (executor_tracker.py)
-  __device__ int32_t source_job() const {  // :98-102
+  __device__ __forceinline__ int32_t source_job() const {  // :98-102
     return (h.source <= kPoolCommon) ? -1 : pool_job(h.source);
   }
-  __device__ int committable() {  // :105-111 (pool None is always empty with no commitments)
+  __device__ __forceinline__ int committable() {  // :105-111 (pool None is always empty with no commitments)
     if (h.source < 0) return 0;
     const int n = pool_size(h.source) - cfrom(h.source);
     check(n >= 0);
     return n;
   }
-  __device__ int demand(int g) const { return st_rem(g) - (st_mov(g) + st_com(g)); }  // :566-578
+  __device__ __forceinline__ int demand(int g) const { return st_rem(g) - (st_mov(g) + st_com(g)); }  // :566-578
 
-  __device__ void supply_add(int job, int n) {
+  __device__ __forceinline__ void supply_add(int job, int n) {
     if (job < 0)
       h.supply_none += n;
     else
       job_supply(job) += n;
   }
 
-  __device__ void add_commitment(int n, int dst) {  // :146-154, 224-236
+  __device__ __forceinline__ void add_commitment(int n, int dst) {  // :146-154, 224-236
     const int src = h.source;
     check(src >= 0);
     if (src < 0) return;
-    int32_t* cs = F<int32_t>(O.cm_src);
-    int32_t* cd = F<int32_t>(O.cm_dst);
-    int32_t* cc = F<int32_t>(O.cm_cnt);
-    int32_t* co = F<int32_t>(O.cm_ord);
+    int16_t* cs = H<int16_t>(O.cm_src);
+    int16_t* cd = H<int16_t>(O.cm_dst);
+    int16_t* cc = H<int16_t>(O.cm_cnt);
+    int32_t* co = H<int32_t>(O.cm_ord);
     int hit = -1, freeslot = -1;
     for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
       const int k = k0 + W::lane();
@@ -198,12 +220,12 @@ struct Sim {
     }
     W::sync();
     if (hit >= 0) {
-      if (W::lane() == 0) cc[hit] += n;
+      if (W::lane() == 0) cc[hit] = (int16_t)(cc[hit] + n);
     } else if (freeslot >= 0) {
       if (W::lane() == 0) {
-        cs[freeslot] = src;
-        cd[freeslot] = dst;
-        cc[freeslot] = n;
+        cs[freeslot] = (int16_t)src;
+        cd[freeslot] = (int16_t)dst;
+        cc[freeslot] = (int16_t)n;
         co[freeslot] = h.commit_seq;
       }
       h.commit_seq++;
@@ -219,10 +241,10 @@ struct Sim {
     if (dj != sj) supply_add(dj, n);
   }
 
-  __device__ int find_commit(int src, int dst) {
-    const int32_t* cs = F<int32_t>(O.cm_src);
-    const int32_t* cd = F<int32_t>(O.cm_dst);
-    const int32_t* cc = F<int32_t>(O.cm_cnt);
+  __device__ __forceinline__ int find_commit(int src, int dst) {
+    const int16_t* cs = H<int16_t>(O.cm_src);
+    const int16_t* cd = H<int16_t>(O.cm_dst);
+    const int16_t* cc = H<int16_t>(O.cm_cnt);
     for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
       const int k = k0 + W::lane();
       const uint64_t m = W::ballot(k < L.commit_cap && cc[k] > 0 && cs[k] == src && cd[k] == dst);
@@ -231,7 +253,7 @@ struct Sim {
     return -1;
   }
 
-  __device__ int remove_commitment(int e, int dst) {  // :156-173, 238-249; returns src
+  __device__ __forceinline__ int remove_commitment(int e, int dst) {  // :156-173, 238-249; returns src
     const int src = ex_loc(e);
     check(src >= 0);
     const int k = src >= 0 ? find_commit(src, dst) : -1;
@@ -239,11 +261,10 @@ struct Sim {
       fail(SSIM_ERR_INVARIANT);  // ValueError("no commitments from ...") in the reference
       return src;
     }
-    W::sync();
-    int32_t* cc = F<int32_t>(O.cm_cnt);
+    int16_t* cc = H<int16_t>(O.cm_cnt);
     const int left = cc[k] - 1;
     W::sync();
-    if (W::lane() == 0) cc[k] = left;
+    if (W::lane() == 0) cc[k] = (int16_t)left;
     W::sync();
     cfrom(src) -= 1;
     check(cfrom(src) >= 0);
@@ -259,17 +280,17 @@ struct Sim {
     return src;
   }
 
-  __device__ int peek_commitment(int p) {  // :175-180: first key in insertion order, -1 = None
-    const int32_t* cs = F<int32_t>(O.cm_src);
-    const int32_t* cd = F<int32_t>(O.cm_dst);
-    const int32_t* cc = F<int32_t>(O.cm_cnt);
-    const int32_t* co = F<int32_t>(O.cm_ord);
+  __device__ __forceinline__ int peek_commitment(int p) {  // :175-180: first key in insertion order, -1 = None
+    const int16_t* cs = H<int16_t>(O.cm_src);
+    const int16_t* cd = H<int16_t>(O.cm_dst);
+    const int16_t* cc = H<int16_t>(O.cm_cnt);
+    const int32_t* co = H<int32_t>(O.cm_ord);
     int best_ord = 0x7FFFFFFF, best_dst = kPoolNone;
     for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
       const int k = k0 + W::lane();
       const bool ok = k < L.commit_cap && cc[k] > 0 && cs[k] == p;
       int ord = ok ? co[k] : 0x7FFFFFFF;
-      int dst = ok ? cd[k] : kPoolNone;
+      int dst = ok ? (int)cd[k] : kPoolNone;
       W::min_pair(ord, dst);
       if (ord < best_ord) {
         best_ord = ord;
@@ -280,11 +301,11 @@ struct Sim {
   }
 
   // Snapshot of commitments[src] in insertion order into scratch plan: (dst, count) pairs.
-  __device__ int commit_plan(int src, int32_t* plan) {
-    const int32_t* cs = F<int32_t>(O.cm_src);
-    const int32_t* cd = F<int32_t>(O.cm_dst);
-    const int32_t* cc = F<int32_t>(O.cm_cnt);
-    const int32_t* co = F<int32_t>(O.cm_ord);
+  __device__ __forceinline__ int commit_plan(int src, int32_t* plan) {
+    const int16_t* cs = H<int16_t>(O.cm_src);
+    const int16_t* cd = H<int16_t>(O.cm_dst);
+    const int16_t* cc = H<int16_t>(O.cm_cnt);
+    const int32_t* co = H<int32_t>(O.cm_ord);
     int n = 0, last = -1;
     for (;;) {  // selection by increasing insertion stamp (live entries <= N)
       int ord = 0x7FFFFFFF, k_best = -1;
@@ -313,27 +334,46 @@ struct Sim {
     return n;
   }
 
-  __device__ void pool_add(int p, int e) {
-    int32_t* tmp = S<int32_t>(O.sc_keys_b);
-    if (W::lane() == 0) ps_add(pmeta(p), ptab(p), (uint32_t)e, tmp);
+  // CPython-set tables are staged through LDS: one lane-parallel gather of the table, the serial probe
+  // sequence on LDS, one lane-parallel store back.
+  __device__ __forceinline__ uint8_t* stage_table(int p) {
+    uint8_t* t = S<uint8_t>(O.sc_tab_p);
+    const uint8_t* g = ptab(p);
+    const int size = (int)pmeta(p)->mask + 1;
+    W::sync();
+    for (int i = W::lane(); i < size; i += W::kWidth) t[i] = g[i];
+    W::sync();
+    return t;
+  }
+  __device__ __forceinline__ void unstage_table(int p, const uint8_t* t) {
+    W::sync();
+    uint8_t* g = ptab(p);
+    const int size = (int)pmeta(p)->mask + 1;
+    for (int i = W::lane(); i < size; i += W::kWidth) g[i] = t[i];
     W::sync();
   }
-  __device__ void pool_remove(int p, int e) {
+  __device__ __forceinline__ void pool_add(int p, int e) {
+    uint8_t* t = stage_table(p);
+    if (W::lane() == 0) ps_add(pmeta(p), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));
+    unstage_table(p, t);
+  }
+  __device__ __forceinline__ void pool_remove(int p, int e) {
+    uint8_t* t = stage_table(p);
     int ok = 1;
-    if (W::lane() == 0) ok = ps_remove(pmeta(p), ptab(p), (uint32_t)e) ? 1 : 0;
+    if (W::lane() == 0) ok = ps_remove(pmeta(p), t, (uint32_t)e) ? 1 : 0;
     ok = W::bcast_i(ok, 0);
-    W::sync();
+    unstage_table(p, t);
     check(ok != 0);
   }
 
-  __device__ void move_to_pool(int e, int dst, bool send) {  // :186-220
+  __device__ __forceinline__ void move_to_pool(int e, int dst, bool send) {  // :186-220
     const int old = ex_loc(e);
     if (old >= 0) {
       pool_remove(old, e);
       ex_loc(e) = kPoolNone;
     }
     if (!send) {
-      ex_loc(e) = dst;
+      ex_loc(e) = (int16_t)dst;
       pool_add(dst, e);
       return;
     }
@@ -350,12 +390,13 @@ struct Sim {
   }
 
   // Table order of set(e for e in pool.copy() if not busy) — _get_idle_source_executors (:714-728).
-  __device__ int idle_order(int p, int32_t* out) {
+  __device__ __forceinline__ int idle_order(int p, int32_t* out) {
     if (p < 0) return 0;
+    const uint8_t* t = stage_table(p);
     int n = 0;
     if (W::lane() == 0) {
       const PySetMeta* m = pmeta(p);
-      n = ps_keys(m, ptab(p), out);
+      n = ps_keys(m, t, out);
       ps_copy_order(m, out, n, S<uint8_t>(O.sc_tab_a));
       int k = 0;
       for (int i = 0; i < n; ++i)
@@ -369,15 +410,15 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- events (event.py)
-  __device__ void push_event(int e, double t, int type, int g) {
+  __device__ __forceinline__ void push_event(int e, double t, int type, int g) {
     check(ev_seq(e) < 0);  // at most one pending event per executor (DESIGN.md §Event queue)
     ev_t(e) = t;
     ev_seq(e) = h.seq++;
-    ev_type(e) = type;
-    ev_stage(e) = g;
+    ev_type(e) = (int16_t)type;
+    ev_stage(e) = (int16_t)g;
   }
 
-  __device__ void trace(double t, int kind, int e, int job, int sid, int seq) {
+  __device__ __forceinline__ void trace(double t, int kind, int e, int job, int sid, int seq) {
     if (h.trace_len < L.trace_cap && W::lane() == 0) {
       TraceRec* r = reinterpret_cast<TraceRec*>(obs + L.ob_trace) + (int64_t)eid * L.trace_cap + h.trace_len;
       r->t = t;
@@ -392,7 +433,7 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- sampler (tpch.py:75-106, 208-235)
-  __device__ bool draw(int ts, int wave, int level, double* out) {
+  __device__ __forceinline__ bool draw(int ts, int wave, int level, double* out) {
     const int idx = (ts * 3 + wave) * kNumLevels + level;
     const int len = D.dur_len[idx];
     if (len <= 0) return false;  // KeyError (missing) or ValueError (empty): no RNG consumed
@@ -401,7 +442,12 @@ struct Sim {
     return true;
   }
 
-  __device__ double task_duration(int j, int g, int e) {
+  __device__ __forceinline__ static int level_of(double key) {  // EXEC_LEVELS index, -1 if not a level
+    return key == 5.0 ? 0 : key == 10.0 ? 1 : key == 20.0 ? 2 : key == 40.0 ? 3 : key == 50.0 ? 4
+           : key == 60.0 ? 5 : key == 80.0 ? 6 : key == 100.0 ? 7 : -1;
+  }
+
+  __device__ __forceinline__ double task_duration(int j, int g, int e) {
     const int n_local = job_local(j);
     check(n_local > 0);
     const int ts = st_ts(g);
@@ -413,10 +459,7 @@ struct Sim {
       const int pt = 1 + (int)(rng.random() * (hi - lo));
       key = ((double)pt <= (double)n_local - lo) ? lo : hi;
     }
-    int level = -1;
-    const double levels[kNumLevels] = {5, 10, 20, 40, 50, 60, 80, 100};
-    for (int l = 0; l < kNumLevels; ++l)
-      if (key == levels[l]) level = l;
+    int level = level_of(key);
     if (level < 0 || !((D.ts_fw_keymask[ts] >> level) & 1)) level = D.ts_fw_maxlevel[ts];
     double d = 0.0;
     const int last = ex_task(e);
@@ -436,7 +479,7 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- schedulable-stage search (:505-555)
-  __device__ bool stage_pred(int g, int mode, int jx, int src_job) const {
+  __device__ __forceinline__ bool stage_pred(int g, int mode, int jx, int src_job) const {
     const int j = st_job(g);
     if (mode == kScanOnly && j != jx) return false;
     if (mode == kScanExcept && j == jx) return false;
@@ -450,9 +493,9 @@ struct Sim {
   }
 
   // first schedulable stage in node order, or -1
-  __device__ int scan_first(int mode, int jx, int src_job) {
+  __device__ __forceinline__ int scan_first(int mode, int jx, int src_job) {
     const int n = h.n_active_stages;
-    const int32_t* act = F<int32_t>(O.active_stages);
+    const int16_t* act = H<int16_t>(O.active_stages);
     for (int i0 = 0; i0 < n; i0 += W::kWidth) {
       const int i = i0 + W::lane();
       const int g = i < n ? act[i] : -1;
@@ -461,9 +504,9 @@ struct Sim {
     }
     return -1;
   }
-  __device__ bool any_schedulable() { return scan_first(kScanAll, -1, source_job()) >= 0; }
+  __device__ __forceinline__ bool any_schedulable() { return scan_first(kScanAll, -1, source_job()) >= 0; }
 
-  __device__ int find_backup(int e) {  // :821-845 (quirks Q1/Q2)
+  __device__ __forceinline__ int find_backup(int e) {  // :821-845 (quirks Q1/Q2)
     const int jx = ex_job(e);
     check(jx >= 0);
     const int sj = (jx == 0 || jx < 0) ? source_job() : jx;  // `if not source_job_id`
@@ -474,7 +517,7 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- list maintenance
-  __device__ void list_remove(int32_t* list, int n, int value) {  // ordered removal by wave shift
+  __device__ __forceinline__ void list_remove(int16_t* list, int n, int value) {  // ordered removal by wave shift
     int pos = -1;
     for (int i0 = 0; i0 < n && pos < 0; i0 += W::kWidth) {
       const int i = i0 + W::lane();
@@ -485,7 +528,7 @@ struct Sim {
     if (pos < 0) return;
     for (int i0 = pos; i0 < n - 1; i0 += W::kWidth) {
       const int i = i0 + W::lane();
-      const int v = (i < n - 1) ? list[i + 1] : 0;
+      const int16_t v = (i < n - 1) ? list[i + 1] : (int16_t)0;
       W::sync();
       if (i < n - 1) list[i] = v;
       W::sync();
@@ -493,14 +536,14 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- movement state machine
-  __device__ void detach(int j, int e) {  // job.py:84-89
+  __device__ __forceinline__ void detach(int j, int e) {  // job.py:84-89
     check(ex_job(e) == j);
     job_local(j) -= 1;
     ex_job(e) = -1;
     ex_task(e) = -1;
   }
 
-  __device__ void run_next_task(int e, int g) {  // :584-615
+  __device__ __forceinline__ void run_next_task(int e, int g) {  // :584-615
     const int j = st_job(g);
     check(st_rem(g) > 0);
     check(ex_job(e) == j);
@@ -509,13 +552,13 @@ struct Sim {
     st_exe(g) += 1;
     if (st_rem(g) == 0) job_sat(j) += 1;
     const double dur = task_duration(j, g, e);
-    ex_task(e) = g - job_base(j);
+    ex_task(e) = (int16_t)(g - job_base(j));
     ex_busy(e) = 1;
     st_recent(g) = dur;
     push_event(e, h.wall + dur, kEvTask, g);
   }
 
-  __device__ void send(int e, int g) {  // :617-637
+  __device__ __forceinline__ void send(int e, int g) {  // :617-637
     check(!ex_busy(e));
     check(ex_job(e) != st_job(g));
     move_to_pool(e, stage_pool(g), true);
@@ -524,7 +567,7 @@ struct Sim {
   }
 
   // _move_idle_executors (:745-782) with an explicit executor list (n ids in `ids`).
-  __device__ void release_idle_list(int src, const int32_t* ids, int n) {
+  __device__ __forceinline__ void release_idle_list(int src, const int32_t* ids, int n) {
     if (src < 0) src = h.source;
     check(src >= 0);
     if (src <= kPoolCommon) return;
@@ -539,11 +582,11 @@ struct Sim {
       if (dst == kPoolCommon) detach(j, e);
     }
   }
-  __device__ void release_idle_one(int src, int e) {
+  __device__ __forceinline__ void release_idle_one(int src, int e) {
     int32_t one = e;
     release_idle_list(src, &one, 1);
   }
-  __device__ void release_idle_all(int src) {
+  __device__ __forceinline__ void release_idle_all(int src) {
     if (src < 0) src = h.source;
     check(src >= 0);
     if (src <= kPoolCommon) return;
@@ -552,7 +595,7 @@ struct Sim {
     release_idle_list(src, ids, n);
   }
 
-  __device__ void goto_stage(int e, int g) {  // _move_executor_to_stage :799-819 (+ backup loop)
+  __device__ __forceinline__ void goto_stage(int e, int g) {  // _move_executor_to_stage :799-819 (+ backup loop)
     for (int guard = 0; guard < 4 * L.stage_cap + 8; ++guard) {
       if (st_rem(g) == 0) {  // _try_backup_schedule :784-797
         const int b = find_backup(e);
@@ -580,7 +623,7 @@ struct Sim {
     fail(SSIM_ERR_INVARIANT);
   }
 
-  __device__ void fulfill(int e, int dst) {  // :699-712
+  __device__ __forceinline__ void fulfill(int e, int dst) {  // :699-712
     const int src = remove_commitment(e, dst);
     if (dst == kPoolCommon) {
       release_idle_one(src, e);
@@ -589,7 +632,7 @@ struct Sim {
     goto_stage(e, pool_stage(dst));
   }
 
-  __device__ void fulfill_from_source() {  // :730-743
+  __device__ __forceinline__ void fulfill_from_source() {  // :730-743
     int32_t* idle = S<int32_t>(O.sc_keys_a);
     int32_t* plan = S<int32_t>(O.sc_plan);
     const int n_idle = idle_order(h.source, idle);
@@ -608,12 +651,12 @@ struct Sim {
     check(k == n_idle);
   }
 
-  __device__ void commit_leftovers() {  // :487-503
+  __device__ __forceinline__ void commit_leftovers() {  // :487-503
     const int n = committable();
     if (n > 0) add_commitment(n, kPoolCommon);
   }
 
-  __device__ bool release(int e, int g, bool changed) {  // _handle_released_executor :639-660
+  __device__ __forceinline__ bool release(int e, int g, bool changed) {  // _handle_released_executor :639-660
     const int dst = peek_commitment(stage_pool(g));
     if (dst != kPoolNone) {
       fulfill(e, dst);
@@ -625,12 +668,12 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- event handlers (:428-483)
-  __device__ void on_job_arrival(int j) {
+  __device__ __forceinline__ void on_job_arrival(int j) {
     job_state(j) = kJobActive;
     job_arr_dec(j) = h.decisions;
-    int32_t* aj = F<int32_t>(O.active_jobs);
-    int32_t* as = F<int32_t>(O.active_stages);
-    if (W::lane() == 0) aj[h.n_active_jobs] = j;
+    int16_t* aj = H<int16_t>(O.active_jobs);
+    int16_t* as = H<int16_t>(O.active_stages);
+    if (W::lane() == 0) aj[h.n_active_jobs] = (int16_t)j;
     const int base = job_base(j), n = job_nst(j);
     for (int k0 = 0; k0 <= n; k0 += W::kWidth) {  // pools of the job and its stages, active-stage list
       const int k = k0 + W::lane();
@@ -638,7 +681,7 @@ struct Sim {
         const int p = (k == n) ? job_pool(j) : stage_pool(base + k);
         ps_init(pmeta(p), ptab(p));
         cfrom(p) = 0;
-        if (k < n) as[h.n_active_stages + k] = base + k;
+        if (k < n) as[h.n_active_stages + k] = (int16_t)(base + k);
       }
     }
     W::sync();
@@ -647,20 +690,20 @@ struct Sim {
     if (pool_size(kPoolCommon) > 0) h.source = kPoolCommon;
   }
 
-  __device__ void on_executor_arrival(int e, int g) {  // :440-450
+  __device__ __forceinline__ void on_executor_arrival(int e, int g) {  // :440-450
     const int j = st_job(g);
     check(ex_task(e) < 0);  // Job.attach_executor asserts executor.task is None
     job_local(j) += 1;
-    ex_job(e) = j;
+    ex_job(e) = (int16_t)j;
     st_mov(g) -= 1;
     check(st_mov(g) >= 0);
     move_to_pool(e, job_pool(j), false);
     goto_stage(e, g);
   }
 
-  __device__ bool stage_completed(int j, int g) {  // Job.record_stage_completion (job.py:65-73,113-128)
+  __device__ __forceinline__ bool stage_completed(int j, int g) {  // Job.record_stage_completion (job.py:65-73,113-128)
     check(st_unmet(g) == 0);  // frontier_stages.remove(stage)
-    list_remove(F<int32_t>(O.active_stages), h.n_active_stages, g);
+    list_remove(H<int16_t>(O.active_stages), h.n_active_stages, g);
     h.n_active_stages -= 1;
     job_nact(j) -= 1;
     const int ts = st_ts(g), base = job_base(j);
@@ -673,10 +716,10 @@ struct Sim {
     return changed;
   }
 
-  __device__ void job_completed(int j) {  // :682-697
+  __device__ __forceinline__ void job_completed(int j) {  // :682-697
     if (pool_size(job_pool(j)) > 0) release_idle_all(job_pool(j));
     check(pool_size(job_pool(j)) == 0);
-    list_remove(F<int32_t>(O.active_jobs), h.n_active_jobs, j);
+    list_remove(H<int16_t>(O.active_jobs), h.n_active_jobs, j);
     h.n_active_jobs -= 1;
     h.n_completed += 1;
     job_state(j) = kJobDone;
@@ -685,11 +728,10 @@ struct Sim {
     trace(h.wall, kTrJobDone, -1, j, -1, -1);
   }
 
-  __device__ void on_task_done(int e, int g) {  // :452-483
+  __device__ __forceinline__ void on_task_done(int e, int g) {  // :452-483
     const int j = st_job(g);
     check(!st_completed(g));
     st_exe(g) -= 1;
-    st_done(g) += 1;
     ex_busy(e) = 0;
     if (st_rem(g) > 0) {
       run_next_task(e, g);
@@ -706,7 +748,7 @@ struct Sim {
   }
 
   // Pops the min (t, seq) event: arrival cursor vs. per-executor slots. Returns false when empty.
-  __device__ bool pop_event(double* t, int* kind, int* e, int* g, int* seq) {
+  __device__ __forceinline__ bool pop_event(double* t, int* kind, int* e, int* g, int* seq) {
     double bt = 0.0;
     int bseq = 0x7FFFFFFF, be = -1;
     for (int k0 = 0; k0 < L.num_executors; k0 += W::kWidth) {
@@ -747,7 +789,7 @@ struct Sim {
   }
 
   // Returns true when it stopped at a decision point (committable executors and a schedulable stage).
-  __device__ bool simulate() {  // _resume_simulation :320-343
+  __device__ __forceinline__ bool simulate() {  // _resume_simulation :320-343
     h.step_events = 0;
     for (;;) {
       if (frozen()) return false;
@@ -788,7 +830,7 @@ struct Sim {
     }
   }
 
-  __device__ double jobtime(double t0, int dec) {  // _compute_jobtime :847-874
+  __device__ __forceinline__ double jobtime(double t0, int dec) {  // _compute_jobtime :847-874
     const double span = h.wall - t0;
     if (span == 0.0) return 0.0;
     double part = 0.0;
@@ -816,12 +858,12 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- observation (:345-406, utils.py)
-  __device__ void observe(double reward) {
+  __device__ __forceinline__ void observe(double reward) {
     const int n = h.n_active_stages;
     const int src_job = source_job();
-    const int32_t* act = F<int32_t>(O.active_stages);
-    int32_t* sched = F<int32_t>(O.sched_list);
-    int32_t* row_of = S<int32_t>(O.sc_row_of);
+    const int16_t* act = H<int16_t>(O.active_stages);
+    int16_t* sched = H<int16_t>(O.sched_list);
+    int16_t* row_of = S<int16_t>(O.sc_row_of);
     float* nodes = reinterpret_cast<float*>(obs + L.ob_nodes) + (int64_t)eid * L.stage_cap * 3;
     uint8_t* front = obs + L.ob_frontier + (int64_t)eid * L.stage_cap;
     int32_t* srank = reinterpret_cast<int32_t*>(obs + L.ob_sched_rank) + (int64_t)eid * L.stage_cap;
@@ -839,15 +881,15 @@ struct Sim {
         nodes[3 * i + 2] = s ? 1.0f : 0.0f;
         front[i] = st_unmet(g) == 0 ? 1 : 0;
         srank[i] = s ? r : -1;
-        row_of[g] = i;
-        if (s) sched[r] = g;
+        row_of[g] = (int16_t)i;
+        if (s) sched[r] = (int16_t)g;
       }
       nsched += W::popc(m);
     }
     W::sync();
     // jobs: dag_ptr, exec_supplies, source_job_idx
     const int nj = h.n_active_jobs;
-    const int32_t* aj = F<int32_t>(O.active_jobs);
+    const int16_t* aj = H<int16_t>(O.active_jobs);
     int32_t* ptr = reinterpret_cast<int32_t*>(obs + L.ob_dag_ptr) + (int64_t)eid * (L.job_cap + 1);
     int32_t* sup = reinterpret_cast<int32_t*>(obs + L.ob_supplies) + (int64_t)eid * L.job_cap;
     int src_idx = nj, run = 0;
@@ -936,7 +978,7 @@ struct Sim {
     W::sync();
   }
 
-  __device__ void write_err_only(uint32_t transient) {
+  __device__ __forceinline__ void write_err_only(uint32_t transient) {
     W::sync();
     if (W::lane() == 0) {
       int32_t* cnts = reinterpret_cast<int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
@@ -946,7 +988,8 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- step (:188-221, :275-315)
-  __device__ void step(StepIn a) {
+  // Requires the hot block in place (load_hot() by the caller for LDS residency).
+  __device__ __forceinline__ void step(StepIn a) {
     load_header();
     if (h.terminated || frozen() || h.num_jobs == 0) return;
     SSIM_TIC(t_act);
@@ -963,7 +1006,7 @@ struct Sim {
         write_err_only(SSIM_ERR_KEY);
         return;
       }
-      const int g = F<int32_t>(O.sched_list)[idx];
+      const int g = H<int16_t>(O.sched_list)[idx];
       if (nx > committable()) {
         write_err_only(SSIM_ERR_TOO_MANY);
         return;
@@ -973,8 +1016,12 @@ struct Sim {
       check(n > 0);
       add_commitment(n, stage_pool(g));
       st_sel(g) = 1;
-      if (W::lane() == 0) F<int32_t>(O.sel_list)[h.n_selected] = g;
-      h.n_selected++;
+      if (h.n_selected <= L.num_executors) {
+        if (W::lane() == 0) H<int16_t>(O.sel_list)[h.n_selected] = (int16_t)g;
+        h.n_selected++;
+      } else {
+        fail(SSIM_ERR_CAPACITY);
+      }
       W::sync();
     }
     h.decisions++;
@@ -996,7 +1043,7 @@ struct Sim {
     SSIM_TOC(t_f, kPhFulfill);
     h.source = kPoolNone;
     {  // selected_stages.clear()
-      const int32_t* sl = F<int32_t>(O.sel_list);
+      const int16_t* sl = H<int16_t>(O.sel_list);
       for (int k0 = 0; k0 < h.n_selected; k0 += W::kWidth) {
         const int k = k0 + W::lane();
         if (k < h.n_selected) st_sel(sl[k]) = 0;
@@ -1018,16 +1065,15 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- reset (:127-186, :260-273)
-  __device__ void reset(const uint8_t* rec_base) {
+  // Runs with the hot block in HBM (hot == ghot).
+  __device__ __forceinline__ void reset(const uint8_t* rec_base) {
     const ssim_reset_record* rec = reinterpret_cast<const ssim_reset_record*>(rec_base);
     const double* tarr = reinterpret_cast<const double*>(rec_base + kResetHeadBytes);
     const int32_t* tpl = reinterpret_cast<const int32_t*>(rec_base + kResetHeadBytes + 8 * (int64_t)L.job_cap);
     const int nj = rec->num_jobs;
     if (nj <= 0) return;
-    const int prev_episode = F<EnvHeader>(O.hdr)->episode;
-    EnvHeader z;
-    memset(&z, 0, sizeof(z));
-    h = z;
+    const int prev_episode = H<EnvHeader>(O.hdr)->episode;
+    h = EnvHeader();
     h.episode = prev_episode + 1;
     h.time_limit = rec->time_limit;
     rng.s_hi = rec->rng_state_hi;
@@ -1059,10 +1105,10 @@ struct Sim {
       int total = 0;
       const int ex = W::excl_scan(ns, &total);
       if (ok) {
-        job_tpl(j) = t;
-        job_base(j) = run + ex;
-        job_nst(j) = ns;
-        job_nact(j) = ns;
+        job_tpl(j) = (int16_t)t;
+        job_base(j) = (int16_t)(run + ex);
+        job_nst(j) = (int16_t)ns;
+        job_nact(j) = (int16_t)ns;
         job_sat(j) = 0;
         job_local(j) = 0;
         job_supply(j) = 0;
@@ -1090,14 +1136,13 @@ struct Sim {
         const int k = k0 + W::lane();
         if (k < ns) {
           const int g = base + k, ts = tsb + k;
-          st_job(g) = j;
-          st_ts(g) = ts;
-          st_rem(g) = D.ts_num_tasks[ts];
+          st_job(g) = (int16_t)j;
+          st_ts(g) = (int16_t)ts;
+          st_rem(g) = (int16_t)D.ts_num_tasks[ts];
           st_exe(g) = 0;
-          st_done(g) = 0;
           st_mov(g) = 0;
           st_com(g) = 0;
-          st_unmet(g) = D.ts_parent_base[ts + 1] - D.ts_parent_base[ts];
+          st_unmet(g) = (int16_t)(D.ts_parent_base[ts + 1] - D.ts_parent_base[ts]);
           st_sel(g) = 0;
           st_recent(g) = D.ts_rough[ts];
         }
@@ -1119,13 +1164,17 @@ struct Sim {
     }
     for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
       const int k = k0 + W::lane();
-      if (k < L.commit_cap) F<int32_t>(O.cm_cnt)[k] = 0;
+      if (k < L.commit_cap) H<int16_t>(O.cm_cnt)[k] = 0;
     }
     W::sync();
-    if (W::lane() == 0) {
-      ps_init(pmeta(kPoolCommon), ptab(kPoolCommon));
-      for (int e = 0; e < L.num_executors; ++e)
-        ps_add(pmeta(kPoolCommon), ptab(kPoolCommon), (uint32_t)e, S<int32_t>(O.sc_keys_b));
+    {
+      uint8_t* t = S<uint8_t>(O.sc_tab_p);
+      if (W::lane() == 0) {
+        ps_init(pmeta(kPoolCommon), t);
+        for (int e = 0; e < L.num_executors; ++e)
+          ps_add(pmeta(kPoolCommon), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));
+      }
+      unstage_table(kPoolCommon, t);
     }
     cfrom(kPoolCommon) = 0;
     W::sync();

@@ -32,22 +32,22 @@ struct PolicyView {
   const uint8_t* obs;
   int eid;
 
-  __device__ const int32_t* counts() const {
+  __device__ __forceinline__ const int32_t* counts() const {
     return reinterpret_cast<const int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
   }
-  __device__ const int32_t* ptr() const {
+  __device__ __forceinline__ const int32_t* ptr() const {
     return reinterpret_cast<const int32_t*>(obs + L.ob_dag_ptr) + (int64_t)eid * (L.job_cap + 1);
   }
-  __device__ const int32_t* sup() const {
+  __device__ __forceinline__ const int32_t* sup() const {
     return reinterpret_cast<const int32_t*>(obs + L.ob_supplies) + (int64_t)eid * L.job_cap;
   }
-  __device__ const int32_t* srank() const {
+  __device__ __forceinline__ const int32_t* srank() const {
     return reinterpret_cast<const int32_t*>(obs + L.ob_sched_rank) + (int64_t)eid * L.stage_cap;
   }
-  __device__ const uint8_t* front() const { return obs + L.ob_frontier + (int64_t)eid * L.stage_cap; }
+  __device__ __forceinline__ const uint8_t* front() const { return obs + L.ob_frontier + (int64_t)eid * L.stage_cap; }
 
   // find_stage (utils.py:17-37) for active job index k; -1 if none
-  __device__ int find_stage(int k) const {
+  __device__ __forceinline__ int find_stage(int k) const {
     const int32_t* p = ptr();
     const int32_t* r = srank();
     const uint8_t* f = front();
@@ -61,7 +61,7 @@ struct PolicyView {
     return fallback;
   }
 
-  __device__ StepIn act(int kind, uint64_t seed, uint64_t counter) const {
+  __device__ __forceinline__ StepIn act(int kind, uint64_t seed, uint64_t counter) const {
     const int32_t* c = counts();
     const int nj = c[SSIM_OC_NUM_JOBS], comm = c[SSIM_OC_COMMITTABLE], src = c[SSIM_OC_SOURCE_JOB_IDX];
     const int N = L.num_executors;

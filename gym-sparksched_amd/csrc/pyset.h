@@ -18,15 +18,16 @@ namespace ssim {
 constexpr uint8_t kSlotEmpty = 0xFF;
 constexpr uint8_t kSlotDummy = 0xFE;
 
+// table metadata of one set (layout.h keeps pools' metadata in the hot block, 6 bytes each)
 struct PySetMeta {
-  uint16_t mask, fill, used, pad;
+  uint16_t mask, fill, used;
 };
+static_assert(sizeof(PySetMeta) == 6, "pool metadata is 6 bytes in the hot block");
 
 __device__ __forceinline__ void ps_init(PySetMeta* m, uint8_t* tab) {
   m->mask = 7;
   m->fill = 0;
   m->used = 0;
-  m->pad = 0;
   for (int i = 0; i < 8; ++i) tab[i] = kSlotEmpty;
 }
 

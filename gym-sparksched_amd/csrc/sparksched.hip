@@ -79,10 +79,17 @@ struct WaveHip {
 // ------------------------------------------------------------------------------------------ kernels
 extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
 
+// An env whose header says terminated / frozen / never reset is skipped without touching LDS.
+__device__ __forceinline__ bool env_idle(const Params* __restrict__ P, const uint8_t* state, int eid) {
+  const EnvHeader* gh =
+      reinterpret_cast<const EnvHeader*>(state + kParamsReserve + (int64_t)eid * P->L.env_bytes + P->O.hdr);
+  return gh->terminated || (gh->err & SSIM_ERR_STICKY) || gh->num_jobs == 0;
+}
+
 __global__ __launch_bounds__(64) void k_reset(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                               const uint8_t* __restrict__ reset) {
   const int eid = blockIdx.x;
-  Sim<WaveHip> s(P, state, g_smem, obs, eid);
+  Sim<WaveHip> s(P, state, g_smem, obs, eid, false);
   s.reset(reset + (int64_t)eid * P->L.reset_stride);
 }
 
@@ -90,11 +97,14 @@ __global__ __launch_bounds__(64) void k_step(const Params* __restrict__ P, uint8
                                              const int32_t* __restrict__ stage_idx,
                                              const int32_t* __restrict__ num_exec) {
   const int eid = blockIdx.x;
-  Sim<WaveHip> s(P, state, g_smem, obs, eid);
+  if (env_idle(P, state, eid)) return;
+  Sim<WaveHip> s(P, state, g_smem, obs, eid, P->O.lds_resident != 0);
   StepIn a;
   a.stage_idx = stage_idx[eid];
   a.num_exec = num_exec[eid];
+  s.load_hot();
   s.step(a);
+  s.save_hot();
 }
 
 __global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, const uint8_t* obs, int kind,
@@ -114,10 +124,12 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
                                                 uint64_t* prof_out) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
-  Sim<WaveHip> s(P, state, g_smem, obs, eid);
+  if (env_idle(P, state, eid) && action_log == nullptr) return;
+  Sim<WaveHip> s(P, state, g_smem, obs, eid, P->O.lds_resident != 0);
   PolicyView<WaveHip> v{P->L, obs, eid};
+  s.load_hot();
+  const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.hot + P->O.hdr);
   for (int k = 0; k < num_steps; ++k) {
-    const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.env + P->O.hdr);
 #ifdef SSIM_PROFILE
     const uint64_t t0 = WaveHip::clock();
 #endif
@@ -132,12 +144,22 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
     WaveHip::sync();
     s.step(a);
   }
+  s.save_hot();
 #ifdef SSIM_PROFILE
   if (prof_out != nullptr && WaveHip::lane() == 0)
     for (int p = 0; p < kNumPhases; ++p) prof_out[(int64_t)eid * kNumPhases + p] = s.prof[p];
 #else
   (void)prof_out;
 #endif
+}
+
+// job state (int16 in the hot block) -> int32 [num_envs][job_cap]
+__global__ __launch_bounds__(64) void k_job_state(const Params* __restrict__ P, const uint8_t* state,
+                                                  int32_t* out) {
+  const int eid = blockIdx.x, J = P->L.job_cap;
+  const int16_t* js =
+      reinterpret_cast<const int16_t*>(state + kParamsReserve + (int64_t)eid * P->L.env_bytes + P->O.job_state);
+  for (int j = threadIdx.x; j < J; j += 64) out[(int64_t)eid * J + j] = js[j];
 }
 
 // ------------------------------------------------------------------------------------------ C ABI
@@ -163,8 +185,6 @@ static int hip_check(hipError_t e, const char* what) {
   return SSIM_OK;
 }
 
-static const int64_t kMaxDynLds = 64 * 1024;
-
 extern "C" int ssim_layout_for(const ssim_config* cfg, ssim_layout* out) {
   StateOffsets O;
   if (cfg == nullptr || out == nullptr || !compute_layout(*cfg, out, &O))
@@ -182,10 +202,14 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
     delete h;
     return set_err(SSIM_E_ARG, "ssim_create: invalid config");
   }
-  if (h->params.L.scratch_bytes > kMaxDynLds) {
+  if (h->params.O.lds_bytes > kLdsBudget) {
     delete h;
-    return set_err(SSIM_E_ARG, "ssim_create: per-env scratch %lld B exceeds LDS budget",
-                   (long long)h->params.L.scratch_bytes);
+    return set_err(SSIM_E_ARG, "ssim_create: per-env scratch %lld B exceeds the LDS budget",
+                   (long long)h->params.O.lds_bytes);
+  }
+  if (dataset->num_template_stages >= 32768 || dataset->num_templates >= 32768) {
+    delete h;
+    return set_err(SSIM_E_ARG, "ssim_create: dataset too large for int16 stage/template ids");
   }
   h->params.D = *dataset;
   h->params.C = *cfg;
@@ -223,7 +247,7 @@ extern "C" int ssim_reset(ssim_handle* h, void* stream) {
 extern "C" int ssim_step(ssim_handle* h, const int32_t* stage_idx, const int32_t* num_exec, void* stream) {
   if (h == nullptr || stage_idx == nullptr || num_exec == nullptr) return set_err(SSIM_E_ARG, "ssim_step: null");
   const ssim_layout& L = h->params.L;
-  hipLaunchKernelGGL(k_step, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_step, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, stage_idx, num_exec);
   return hip_check(hipGetLastError(), "k_step launch");
 }
@@ -245,7 +269,7 @@ extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t
   if (kind != SSIM_POLICY_FAIR && kind != SSIM_POLICY_FIFO && kind != SSIM_POLICY_RANDOM)
     return set_err(SSIM_E_ARG, "ssim_rollout: unknown policy %d", kind);
   const ssim_layout& L = h->params.L;
-  hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, action_log, (uint64_t*)nullptr);
   return hip_check(hipGetLastError(), "k_rollout launch");
 }
@@ -255,7 +279,7 @@ extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t
 extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
                                      uint64_t* prof_out, void* stream) {
   const ssim_layout& L = h->params.L;
-  hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, (int32_t*)nullptr, prof_out);
   return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
 }
@@ -275,9 +299,10 @@ extern "C" int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_compl
   if (rc == SSIM_OK && t_completed)
     rc = hip_check(hipMemcpy2DAsync(t_completed, J * 8, base + O.job_tdone, pitch, J * 8, B, hipMemcpyDeviceToDevice, s),
                    "job t_completed copy");
-  if (rc == SSIM_OK && state)
-    rc = hip_check(hipMemcpy2DAsync(state, J * 4, base + O.job_state, pitch, J * 4, B, hipMemcpyDeviceToDevice, s),
-                   "job state copy");
+  if (rc == SSIM_OK && state) {
+    hipLaunchKernelGGL(k_job_state, dim3(L.num_envs), dim3(64), 0, s, dparams(h), h->state, state);
+    rc = hip_check(hipGetLastError(), "k_job_state launch");
+  }
   return rc;
 }
 

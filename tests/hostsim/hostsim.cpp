@@ -11,6 +11,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+struct uint4 {  // HIP vector type used by the (device-only) LDS residency copy; never taken on the host
+  unsigned x, y, z, w;
+};
+
 #include "engine.h"
 #include "policy.h"
 
@@ -81,7 +85,7 @@ uint8_t* hs_state(hs_handle* h) { return h->state; }
 int hs_reset(hs_handle* h) {
   const Params* P = h->params;
   for (int e = 0; e < P->L.num_envs; ++e) {
-    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e);
+    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
     s.reset(h->reset + (int64_t)e * P->L.reset_stride);
   }
   return 0;
@@ -90,7 +94,7 @@ int hs_reset(hs_handle* h) {
 int hs_step(hs_handle* h, const int32_t* stage_idx, const int32_t* num_exec) {
   const Params* P = h->params;
   for (int e = 0; e < P->L.num_envs; ++e) {
-    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e);
+    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
     StepIn a;
     a.stage_idx = stage_idx[e];
     a.num_exec = num_exec[e];
@@ -114,10 +118,10 @@ int hs_rollout(hs_handle* h, int kind, uint64_t seed, int num_steps, int32_t* ac
   const Params* P = h->params;
   const int B = P->L.num_envs;
   for (int e = 0; e < B; ++e) {
-    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e);
+    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
     PolicyView<WaveSerial> v{P->L, h->obs, e};
     for (int k = 0; k < num_steps; ++k) {
-      const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.env + P->O.hdr);
+      const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.hot + P->O.hdr);
       const StepIn a = v.act(kind, seed, (uint64_t)hd->decisions + ((uint64_t)hd->episode << 32));
       if (action_log) {
         action_log[((int64_t)k * B + e) * 2 + 0] = a.stage_idx;
@@ -136,7 +140,8 @@ void hs_job_times(hs_handle* h, double* ta, double* tc, int32_t* st) {
     const uint8_t* env = h->state + kParamsReserve + (int64_t)e * P->L.env_bytes;
     memcpy(ta + (int64_t)e * J, env + P->O.job_tarr, 8 * (size_t)J);
     memcpy(tc + (int64_t)e * J, env + P->O.job_tdone, 8 * (size_t)J);
-    memcpy(st + (int64_t)e * J, env + P->O.job_state, 4 * (size_t)J);
+    const int16_t* js = reinterpret_cast<const int16_t*>(env + P->O.job_state);
+    for (int j = 0; j < J; ++j) st[(int64_t)e * J + j] = js[j];
   }
 }
 
