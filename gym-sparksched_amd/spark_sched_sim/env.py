@@ -1,0 +1,153 @@
+"""Single-env drop-in for spark_sched_sim.SparkSchedSimEnv (reference spark_sched_sim/spark_sched_sim.py:29-245).
+
+Same constructor config keys, `reset(seed, options) -> (obs, info)`, `step(action) -> (obs, reward,
+terminated, truncated, info)`, observation dicts (GraphInstance(nodes f32[S,3], edges i64[E], edge_links
+i64[E,2]), dag_ptr, num_committable_execs, source_job_idx, exec_supplies), action-space bookkeeping and
+exception types (ValueError / KeyError / AssertionError). The state machine runs on the GPU (one
+wavefront); this class only marshals one env's slice of the obs arena to numpy.
+"""
+
+from __future__ import annotations
+
+import math
+from collections import deque
+from typing import Any
+
+import numpy as np
+
+from . import _abi
+from .engine import DeviceEngine, obs_dict
+from .spaces import ActionSpace
+
+NUM_NODE_FEATURES = 3
+
+
+def _raise_for(err: int, action) -> None:
+    if err & _abi.SSIM_ERR_SPACE:
+        raise ValueError("invalid action: does not belong to the action space")
+    if err & _abi.SSIM_ERR_KEY:
+        raise KeyError(action["stage_idx"])
+    if err & _abi.SSIM_ERR_TOO_MANY:
+        raise ValueError("invalid action: too many executors requested")
+    if err & _abi.SSIM_ERR_SAMPLER:
+        raise ValueError("task_duration: no duration data for the sampled executor key")
+    if err & _abi.SSIM_ERR_INVARIANT:
+        raise AssertionError("simulator invariant violated (reference `assert`)")
+    if err & (_abi.SSIM_ERR_CAPACITY | _abi.SSIM_ERR_RESET):
+        raise RuntimeError(f"device capacity/reset error {err:#x}")
+
+
+class SparkSchedSimEnv:
+    """A Gymnasium-style env that simulates DAG job scheduling in Spark, stepped on the GPU."""
+
+    metadata = {"render_modes": ["human"], "render_fps": 30}
+
+    def __init__(self, env_cfg: dict[str, Any], dataset=None, device="cuda", job_cap: int | None = None,
+                 _engine_factory=None):
+        self.num_executors: int = env_cfg["num_executors"]
+        self.moving_delay = env_cfg["moving_delay"]
+        self.beta = env_cfg.get("beta", 0)
+        self.job_arrival_cap = env_cfg.get("job_arrival_cap")
+        self.render_mode = env_cfg.get("render_mode")
+        if self.render_mode == "human":
+            raise ValueError("pygame is unavailable")  # rendering is out of scope (no renderer is built)
+        sampler = env_cfg.get("data_sampler_cls", "TPCHDataSampler")
+        if sampler != "TPCHDataSampler":
+            raise AssertionError(f"'{sampler}' is not a valid data sampler.")
+        if dataset is None:
+            from .data_samplers.synthetic_tpch import generate
+
+            dataset = generate(0)
+        factory = _engine_factory or (lambda cfg, ds: DeviceEngine(cfg, 1, ds, device=device, job_cap=job_cap))
+        self._eng = factory(dict(env_cfg), dataset)
+        self.action_space = ActionSpace(self.num_executors)
+        self.job_duration_buff: deque = deque(maxlen=200)
+        self.wall_time = 0.0
+        self._obs = None
+        self._have_episode = False
+
+    # -- gym API ------------------------------------------------------------------------------------
+    def reset(self, seed: int | None = None, options: dict | None = None):
+        if self._have_episode:
+            self._flush_durations()
+        self._eng.reset(seeds=[seed] if seed is not None else None, options=options)
+        self._have_episode = True
+        v = self._eng.host_views()
+        err = int(v["counts"][0][_abi.OC_ERR])
+        if err:
+            _raise_for(err, {"stage_idx": None})
+        self.job_arrival_cap = self._eng.sampler.arrival_cap[0]
+        return self._observe(v), self.info
+
+    def step(self, action: dict):
+        if not self.action_space.contains(action):
+            raise ValueError("invalid action: does not belong to the action space")
+        self._eng.step([int(action["stage_idx"])], [int(action["num_exec"])])
+        v = self._eng.host_views()
+        c = v["counts"][0]
+        err = int(c[_abi.OC_ERR])
+        if err:
+            _raise_for(err, action)
+        obs = self._observe(v)
+        return obs, float(v["reward"][0]), bool(c[_abi.OC_TERMINATED]), False, self.info
+
+    def close(self) -> None:
+        self._eng.close()
+
+    # -- reference properties (spark_sched_sim.py:227-245) ------------------------------------------
+    @property
+    def info(self) -> dict:
+        return {"wall_time": self.wall_time}
+
+    @property
+    def all_jobs_complete(self) -> bool:
+        c = self._counts()
+        return int(c[_abi.OC_NUM_COMPLETED]) == self.job_arrival_cap
+
+    @property
+    def num_completed_jobs(self) -> int:
+        return int(self._counts()[_abi.OC_NUM_COMPLETED])
+
+    @property
+    def num_active_jobs(self) -> int:
+        return int(self._counts()[_abi.OC_NUM_JOBS])
+
+    @property
+    def avg_job_duration(self) -> float:
+        return np.mean(list(self.job_duration_buff) + self._episode_durations()).item() * 1e-3
+
+    def job_times(self):
+        """(t_arrival, t_completed, state) numpy arrays of this episode's jobs."""
+        ta, tc, st = self._eng.job_times_np()
+        n = int(self._counts()[_abi.OC_NUM_ARRIVED]) if self._have_episode else 0
+        total = self.job_arrival_cap or 0
+        return ta[0][:total], tc[0][:total], st[0][:total], n
+
+    # -- internals ----------------------------------------------------------------------------------
+    def _counts(self):
+        return self._eng.host_views()["counts"][0]
+
+    def _observe(self, v):
+        obs = obs_dict(v, 0)
+        self.wall_time = float(v["wall_time"][0])
+        self.action_space["stage_idx"].n = obs["dag_batch"].nodes.shape[0] + 1
+        return obs
+
+    def _episode_durations(self):
+        ta, tc, st, _ = self.job_times()
+        done = np.nonzero(st == 2)[0]
+        order = done[np.argsort(tc[done], kind="stable")]
+        return [float(tc[j] - ta[j]) for j in order]
+
+    def _flush_durations(self):
+        for d in self._episode_durations():
+            self.job_duration_buff.append(d)
+
+
+def make(env_cfg: dict, **kw) -> SparkSchedSimEnv:
+    """gym.make("spark_sched_sim:SparkSchedSimEnv-v0", env_cfg=...) equivalent (spark_sched_sim/__init__.py:6)."""
+    return SparkSchedSimEnv(env_cfg, **kw)
+
+
+def time_limit_from(options) -> float:
+    return math.inf if not options else options.get("time_limit", math.inf)

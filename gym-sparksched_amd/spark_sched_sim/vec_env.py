@@ -1,0 +1,89 @@
+"""Batched env: B independent SparkSchedSimEnv instances on one GPU with torch device tensors.
+
+Observations are zero-copy views of the obs arena (padded per env; `num_nodes`/`num_edges`/`num_jobs`
+give the valid prefix). They are overwritten by the next step — consumers that keep observations (rollout
+storage) copy them. Actions are device int32 tensors `stage_idx[B]`, `num_exec[B]` with the reference's
+meaning (spark_sched_sim.py:275-315). Per-env errors are reported in `info["err"]` (SSIM_ERR_* bits);
+a frozen env (sticky error) stops advancing until its next reset.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi
+from .engine import DeviceEngine
+from .wrappers import StochasticTimeLimitSampler
+
+
+class SparkSchedSimVecEnv:
+    def __init__(self, env_cfg: dict, num_envs: int, dataset=None, device="cuda", job_cap=None,
+                 mean_time_limit: float | None = None, time_limit_seed: int = 42, trace_cap: int = 0):
+        if dataset is None:
+            from .data_samplers.synthetic_tpch import generate
+
+            dataset = generate(0)
+        self.num_envs = num_envs
+        self.num_executors = env_cfg["num_executors"]
+        self.engine = DeviceEngine(env_cfg, num_envs, dataset, device=device, job_cap=job_cap, trace_cap=trace_cap)
+        self.device = self.engine.device
+        self.layout = self.engine.layout
+        self._limits = (StochasticTimeLimitSampler(mean_time_limit, num_envs, time_limit_seed)
+                        if mean_time_limit else None)
+        v = self.engine.views
+        c = v["counts"]
+        self.obs = {
+            "nodes": v["nodes"], "edge_links": v["edge_links"], "dag_ptr": v["dag_ptr"],
+            "exec_supplies": v["exec_supplies"], "frontier": v["frontier"], "sched_rank": v["sched_rank"],
+            "num_nodes": c[:, _abi.OC_NUM_NODES], "num_edges": c[:, _abi.OC_NUM_EDGES],
+            "num_jobs": c[:, _abi.OC_NUM_JOBS], "num_committable_execs": c[:, _abi.OC_COMMITTABLE],
+            "source_job_idx": c[:, _abi.OC_SOURCE_JOB_IDX], "num_schedulable": c[:, _abi.OC_NUM_SCHEDULABLE],
+        }
+
+    def reset(self, seed=None, options=None, env_ids=None):
+        ids = list(range(self.num_envs)) if env_ids is None else list(env_ids)
+        if self._limits is not None:
+            seeds = None if seed is None else ([seed + i for i in ids] if np.isscalar(seed) else list(seed))
+            options = [{"time_limit": self._limits.sample(i, None if seeds is None else seeds[k])}
+                       for k, i in enumerate(ids)]
+        self.engine.reset(seeds=seed, options=options, env_ids=env_ids)
+        return self.obs, self._info()
+
+    def step(self, stage_idx, num_exec):
+        self.engine.step(stage_idx, num_exec)
+        c = self.engine.views["counts"]
+        term = c[:, _abi.OC_TERMINATED] != 0
+        trunc = c[:, _abi.OC_TRUNCATED] != 0
+        return self.obs, self.engine.views["reward"], term, trunc, self._info()
+
+    def policy(self, kind: int = _abi.SSIM_POLICY_FAIR, seed: int = 0, counter: int = 0):
+        """On-device action driver (fair / FIFO / random); returns (stage_idx, num_exec) tensors."""
+        return self.engine.policy(kind, seed, counter)
+
+    def rollout(self, kind: int, seed: int, num_steps: int, action_log=None):
+        """`num_steps` device-policy decisions per env fused into one launch."""
+        self.engine.rollout(kind, seed, num_steps, action_log)
+
+    def _info(self):
+        c = self.engine.views["counts"]
+        return {"wall_time": self.engine.views["wall_time"], "err": c[:, _abi.OC_ERR],
+                "decisions": c[:, _abi.OC_DECISIONS], "num_completed_jobs": c[:, _abi.OC_NUM_COMPLETED]}
+
+    def episode_stats(self):
+        """Per-env stats as in trainers/rollout_worker.py:122-129 (avg job duration over this episode's
+        completed jobs, avg number of jobs in system, completed and arrived job counts), float64 [B, 4]."""
+        import torch
+
+        ta, tc, st = self.engine.job_times()
+        wall = self.engine.views["wall_time"][:, None]
+        arrived = st > 0
+        end = torch.where(st == 2, tc, wall.expand_as(tc))
+        dur = torch.where(arrived, end - ta, torch.zeros_like(ta))
+        n_done = (st == 2).sum(1)
+        done_dur = torch.where(st == 2, dur, torch.zeros_like(dur)).sum(1)
+        avg_jd = done_dur / n_done.clamp(min=1) * 1e-3
+        avg_jobs = dur.sum(1) / wall[:, 0].clamp(min=1e-12)
+        return torch.stack([avg_jd, avg_jobs, n_done.double(), arrived.sum(1).double()], dim=1)
+
+    def close(self):
+        self.engine.close()

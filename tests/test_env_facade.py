@@ -1,0 +1,113 @@
+"""The single-env drop-in facade (spark_sched_sim.env.SparkSchedSimEnv), StochasticTimeLimit and metrics vs the
+CPU oracle. CPU suite: the facade is driven through its engine seam with the test-only host build; the device
+variant of the same checks is in test_gpu_parity.py::test_env_facade_device."""
+
+import numpy as np
+import pytest
+
+import parity
+from oracle import restatement as R
+from oracle.policies import FairPolicy, RandomPolicy
+from spark_sched_sim import metrics
+from spark_sched_sim.env import SparkSchedSimEnv
+from spark_sched_sim.wrappers import StochasticTimeLimit
+
+
+def host_factory(job_cap=None):
+    from hostsim.driver import HostEngine
+
+    return lambda cfg, ds: HostEngine(cfg, 1, ds, job_cap=job_cap)
+
+
+def run_facade_vs_oracle(env, ref, policy_ref, seed, max_steps=100000, options=None):
+    obs, info = env.reset(seed=seed, options=options)
+    robs, rinfo = ref.reset(seed=seed, options=options)
+    parity.compare_obs(robs, obs, "reset")
+    assert info == rinfo or info["wall_time"] == rinfo["wall_time"]
+    done = trunc = False
+    steps = 0
+    while not (done or trunc) and steps < max_steps:
+        a, _ = policy_ref.schedule(robs)
+        obs, r, done, trunc, info = env.step(a)
+        robs, rr, rdone, rtrunc, rinfo = ref.step(a)
+        parity.compare_obs(robs, obs, f"step {steps}")
+        assert parity.close_rel(r, rr) and done == rdone and trunc == rtrunc
+        assert info["wall_time"] == rinfo["wall_time"]
+        steps += 1
+    return steps
+
+
+def test_facade_fair_episode_matches_oracle(dataset, env_cfg):
+    env = SparkSchedSimEnv(env_cfg, dataset, _engine_factory=host_factory())
+    ref = R.SparkSchedOracle(env_cfg, dataset)
+    steps = run_facade_vs_oracle(env, ref, FairPolicy(10), seed=1234)
+    assert steps > 100 and env.all_jobs_complete
+    assert env.num_completed_jobs == len(ref.completed_ids) and env.num_active_jobs == 0
+    assert env.job_arrival_cap == ref.job_arrival_cap
+    assert np.isclose(env.avg_job_duration, ref.avg_job_duration, rtol=1e-12)
+    assert np.isclose(metrics.avg_job_duration(env), R.avg_job_duration(ref), rtol=1e-12)
+    assert np.isclose(metrics.avg_num_jobs(env), R.avg_num_jobs(ref), rtol=1e-12)
+    # second episode: the duration buffer spans resets (deque(maxlen=200), spark_sched_sim.py:83)
+    run_facade_vs_oracle(env, ref, FairPolicy(10), seed=99)
+    assert np.isclose(env.avg_job_duration, ref.avg_job_duration, rtol=1e-12)
+
+
+def test_facade_raises_like_reference(dataset, env_cfg):
+    env = SparkSchedSimEnv(env_cfg, dataset, _engine_factory=host_factory())
+    ref = R.SparkSchedOracle(env_cfg, dataset)
+    obs, _ = env.reset(seed=5)
+    ref.reset(seed=5)
+    n = obs["dag_batch"].nodes.shape[0]
+    bad = [{"stage_idx": n, "num_exec": 1}, {"stage_idx": 0, "num_exec": 0}, {"stage_idx": 0},
+           {"stage_idx": 0.0, "num_exec": 1}, {"stage_idx": np.int64(-2), "num_exec": 1},
+           {"stage_idx": 0, "num_exec": 11}]
+    for a in bad:
+        with pytest.raises(ValueError):
+            env.step(a)
+        with pytest.raises(ValueError):
+            ref.step(a)
+    ns = int(obs["dag_batch"].nodes[:, 2].sum())
+    if ns < n:
+        with pytest.raises(KeyError):
+            env.step({"stage_idx": ns, "num_exec": 1})
+        with pytest.raises(KeyError):
+            ref.step({"stage_idx": ns, "num_exec": 1})
+    # a valid numpy-int action after the failures behaves exactly like the oracle
+    a, _ = FairPolicy(10).schedule(obs)
+    a = {"stage_idx": np.int64(a["stage_idx"]), "num_exec": np.int32(a["num_exec"])}
+    o1, r1, d1, _, _ = env.step(a)
+    o2, r2, d2, _, _ = ref.step(a)
+    parity.compare_obs(o2, o1, "after errors")
+
+
+def test_reset_requires_a_limit(dataset, env_cfg):
+    cfg = dict(env_cfg, job_arrival_cap=None)
+    env = SparkSchedSimEnv(cfg, dataset, job_cap=400, _engine_factory=host_factory(job_cap=400))
+    with pytest.raises(ValueError):
+        env.reset(seed=1)
+    with pytest.raises(ValueError):
+        R.SparkSchedOracle(cfg, dataset).reset(seed=1)
+
+
+def test_stochastic_time_limit_episode(dataset, env_cfg):
+    """Time-limited episode without a job cap (decima_tpch.yaml-style), truncation semantics."""
+    cfg = dict(env_cfg, job_arrival_cap=None)
+    env = StochasticTimeLimit(SparkSchedSimEnv(cfg, dataset, job_cap=400,
+                                               _engine_factory=host_factory(job_cap=400)), 1.5e6, seed=3)
+    ref = StochasticTimeLimit(R.SparkSchedOracle(cfg, dataset), 1.5e6, seed=3)
+    for seed in (17, None):
+        obs, _ = env.reset(seed=seed)
+        robs, _ = ref.reset(seed=seed)
+        assert env.time_limit == ref.time_limit
+        parity.compare_obs(robs, obs, "reset")
+        pol = RandomPolicy(7)
+        done = trunc = False
+        k = 0
+        while not (done or trunc):
+            a, _ = pol.schedule(robs)
+            obs, r, done, trunc, info = env.step(a)
+            robs, rr, rdone, rtrunc, rinfo = ref.step(a)
+            parity.compare_obs(robs, obs, f"step {k}")
+            assert (done, trunc) == (rdone, rtrunc) and parity.close_rel(r, rr)
+            k += 1
+        assert trunc or done
