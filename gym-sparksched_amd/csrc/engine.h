@@ -34,8 +34,9 @@
 
 namespace ssim {
 
+// top-level phases (disjoint) then inclusive sub-timers (nested inside the top-level ones)
 enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kPhHandle, kPhPostScan, kPhObserve,
-                 kNumPhases };
+                 kPhSample, kPhPool, kPhScan, kPhLoadSave, kNumPhases };
 enum : int32_t { kPoolNone = -1, kPoolCommon = 0 };
 enum : int32_t { kEvArrival = 1, kEvTask = 2, kEvReady = 3, kTrJobDone = 4 };
 enum : int32_t { kJobPending = 0, kJobActive = 1, kJobDone = 2 };
@@ -71,7 +72,7 @@ struct Sim {
   EnvHeader h;    // register copy of the header
   Pcg64 rng;
 #ifdef SSIM_PROFILE
-  uint64_t prof[kNumPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t prof[kNumPhases] = {0};
 #endif
 
   // `lds` = this wave's LDS block: [scratch | hot copy (if resident)]; resident=false keeps hot in HBM.
@@ -92,10 +93,14 @@ struct Sim {
     W::sync();
   }
   __device__ __forceinline__ void load_hot() {
+    SSIM_TIC(t0);
     if (hot != ghot) copy16(hot, ghot, O.hot_bytes);
+    SSIM_TOC(t0, kPhLoadSave);
   }
   __device__ __forceinline__ void save_hot() {
+    SSIM_TIC(t0);
     if (hot != ghot) copy16(ghot, hot, O.hot_bytes);
+    SSIM_TOC(t0, kPhLoadSave);
   }
 
   // ---------------------------------------------------------------- field access
@@ -133,39 +138,46 @@ struct Sim {
     if (!ok) h.err |= SSIM_ERR_INVARIANT;
   }
 
-  // stages (env-global index g = job_base[j] + local stage id); `done` is derived: rem + exe + done = tasks
-  __device__ __forceinline__ int16_t& st_job(int g) const { return H<int16_t>(O.st_job)[g]; }
-  __device__ __forceinline__ int16_t& st_ts(int g) const { return H<int16_t>(O.st_ts)[g]; }
-  __device__ __forceinline__ int16_t& st_rem(int g) const { return H<int16_t>(O.st_rem)[g]; }
-  __device__ __forceinline__ int16_t& st_exe(int g) const { return H<int16_t>(O.st_exe)[g]; }
-  __device__ __forceinline__ int16_t& st_mov(int g) const { return H<int16_t>(O.st_mov)[g]; }
-  __device__ __forceinline__ int16_t& st_com(int g) const { return H<int16_t>(O.st_com)[g]; }
-  __device__ __forceinline__ int16_t& st_unmet(int g) const { return H<int16_t>(O.st_unmet)[g]; }
-  __device__ __forceinline__ uint8_t& st_sel(int g) const { return H<uint8_t>(O.st_sel)[g]; }
+  // records (layout.h); accessors keep the algorithm code independent of the record packing
+  __device__ __forceinline__ StageRec& stage(int g) const { return H<StageRec>(O.stages)[g]; }
+  __device__ __forceinline__ JobRec& job(int j) const { return H<JobRec>(O.jobs)[j]; }
+  __device__ __forceinline__ JobTimes& jtimes(int j) const { return H<JobTimes>(O.jtimes)[j]; }
+  __device__ __forceinline__ ExecRec& exr(int e) const { return H<ExecRec>(O.execs)[e]; }
+  __device__ __forceinline__ CommitRec& cm(int k) const { return H<CommitRec>(O.commits)[k]; }
+  __device__ __forceinline__ PoolRec& pool(int p) const { return H<PoolRec>(O.pools)[p]; }
+  // stages (env-global index g = job base + local stage id); `done` is derived: rem + exe + done = tasks
+  __device__ __forceinline__ int16_t& st_job(int g) const { return stage(g).job; }
+  __device__ __forceinline__ int16_t& st_ts(int g) const { return stage(g).ts; }
+  __device__ __forceinline__ int16_t& st_rem(int g) const { return stage(g).rem; }
+  __device__ __forceinline__ int16_t& st_exe(int g) const { return stage(g).exe; }
+  __device__ __forceinline__ int16_t& st_mov(int g) const { return stage(g).mov; }
+  __device__ __forceinline__ int16_t& st_com(int g) const { return stage(g).com; }
+  __device__ __forceinline__ int16_t& st_unmet(int g) const { return stage(g).unmet; }
+  __device__ __forceinline__ uint8_t& st_sel(int g) const { return stage(g).sel; }
   __device__ __forceinline__ double& st_recent(int g) const { return reinterpret_cast<double*>(cold + O.st_recent)[g]; }
   __device__ __forceinline__ bool st_completed(int g) const { return st_rem(g) == 0 && st_exe(g) == 0; }
   // jobs
-  __device__ __forceinline__ int16_t& job_tpl(int j) const { return H<int16_t>(O.job_tpl)[j]; }
-  __device__ __forceinline__ int16_t& job_base(int j) const { return H<int16_t>(O.job_base)[j]; }
-  __device__ __forceinline__ int16_t& job_nst(int j) const { return H<int16_t>(O.job_nst)[j]; }
-  __device__ __forceinline__ int16_t& job_nact(int j) const { return H<int16_t>(O.job_nact)[j]; }
-  __device__ __forceinline__ int16_t& job_sat(int j) const { return H<int16_t>(O.job_sat)[j]; }
-  __device__ __forceinline__ int16_t& job_local(int j) const { return H<int16_t>(O.job_local)[j]; }
-  __device__ __forceinline__ int16_t& job_supply(int j) const { return H<int16_t>(O.job_supply)[j]; }
-  __device__ __forceinline__ int16_t& job_state(int j) const { return H<int16_t>(O.job_state)[j]; }
-  __device__ __forceinline__ int32_t& job_arr_dec(int j) const { return H<int32_t>(O.job_arr_dec)[j]; }
-  __device__ __forceinline__ int32_t& job_done_dec(int j) const { return H<int32_t>(O.job_done_dec)[j]; }
-  __device__ __forceinline__ double& job_tarr(int j) const { return H<double>(O.job_tarr)[j]; }
-  __device__ __forceinline__ double& job_tdone(int j) const { return H<double>(O.job_tdone)[j]; }
+  __device__ __forceinline__ int16_t& job_tpl(int j) const { return job(j).tpl; }
+  __device__ __forceinline__ int16_t& job_base(int j) const { return job(j).base; }
+  __device__ __forceinline__ int16_t& job_nst(int j) const { return job(j).nst; }
+  __device__ __forceinline__ int16_t& job_nact(int j) const { return job(j).nact; }
+  __device__ __forceinline__ int16_t& job_sat(int j) const { return job(j).sat; }
+  __device__ __forceinline__ int16_t& job_local(int j) const { return job(j).local; }
+  __device__ __forceinline__ int16_t& job_supply(int j) const { return job(j).supply; }
+  __device__ __forceinline__ int16_t& job_state(int j) const { return job(j).state; }
+  __device__ __forceinline__ int32_t& job_arr_dec(int j) const { return job(j).arr_dec; }
+  __device__ __forceinline__ int32_t& job_done_dec(int j) const { return job(j).done_dec; }
+  __device__ __forceinline__ double& job_tarr(int j) const { return jtimes(j).tarr; }
+  __device__ __forceinline__ double& job_tdone(int j) const { return jtimes(j).tdone; }
   // executors
-  __device__ __forceinline__ int16_t& ex_loc(int e) const { return H<int16_t>(O.ex_loc)[e]; }
-  __device__ __forceinline__ int16_t& ex_job(int e) const { return H<int16_t>(O.ex_job)[e]; }
-  __device__ __forceinline__ int16_t& ex_task(int e) const { return H<int16_t>(O.ex_task)[e]; }
-  __device__ __forceinline__ int16_t& ex_busy(int e) const { return H<int16_t>(O.ex_busy)[e]; }
-  __device__ __forceinline__ double& ev_t(int e) const { return H<double>(O.ev_t)[e]; }
-  __device__ __forceinline__ int32_t& ev_seq(int e) const { return H<int32_t>(O.ev_seq)[e]; }
-  __device__ __forceinline__ int16_t& ev_type(int e) const { return H<int16_t>(O.ev_type)[e]; }
-  __device__ __forceinline__ int16_t& ev_stage(int e) const { return H<int16_t>(O.ev_stage)[e]; }
+  __device__ __forceinline__ int16_t& ex_loc(int e) const { return exr(e).loc; }
+  __device__ __forceinline__ int16_t& ex_job(int e) const { return exr(e).job; }
+  __device__ __forceinline__ int16_t& ex_task(int e) const { return exr(e).task; }
+  __device__ __forceinline__ int16_t& ex_busy(int e) const { return exr(e).busy; }
+  __device__ __forceinline__ double& ev_t(int e) const { return exr(e).ev_t; }
+  __device__ __forceinline__ int32_t& ev_seq(int e) const { return exr(e).ev_seq; }
+  __device__ __forceinline__ int16_t& ev_type(int e) const { return exr(e).ev_type; }
+  __device__ __forceinline__ int16_t& ev_stage(int e) const { return exr(e).ev_stage; }
   // pools: code 0 = COMMON, 1+j = job j, 1+job_cap+g = stage g, -1 = None
   __device__ __forceinline__ int32_t job_pool(int j) const { return 1 + j; }
   __device__ __forceinline__ int32_t stage_pool(int g) const { return 1 + L.job_cap + g; }
@@ -176,10 +188,10 @@ struct Sim {
     if (p <= L.job_cap) return p - 1;
     return st_job(p - 1 - L.job_cap);
   }
-  __device__ __forceinline__ PySetMeta* pmeta(int p) const { return H<PySetMeta>(O.pool_meta) + p; }
+  __device__ __forceinline__ PySetMeta* pmeta(int p) const { return reinterpret_cast<PySetMeta*>(&pool(p)); }
   __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + O.pool_tab + (int64_t)p * L.set_cap; }
-  __device__ __forceinline__ int16_t& cfrom(int p) const { return H<int16_t>(O.pool_cfrom)[p]; }
-  __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)pmeta(p)->used; }
+  __device__ __forceinline__ int16_t& cfrom(int p) const { return pool(p).cfrom; }
+  __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)pool(p).used; }
 
   // ---------------------------------------------------------------- tracker (executor_tracker.py)
   __device__ __forceinline__ int32_t source_job() const {  // :98-102
@@ -204,29 +216,27 @@ struct Sim {
     const int src = h.source;
     check(src >= 0);
     if (src < 0) return;
-    int16_t* cs = H<int16_t>(O.cm_src);
-    int16_t* cd = H<int16_t>(O.cm_dst);
-    int16_t* cc = H<int16_t>(O.cm_cnt);
-    int32_t* co = H<int32_t>(O.cm_ord);
     int hit = -1, freeslot = -1;
     for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
       const int k = k0 + W::lane();
       const bool ok = k < L.commit_cap;
-      const int cnt = ok ? cc[k] : 0;
-      const uint64_t mh = W::ballot(ok && cnt > 0 && cs[k] == src && cd[k] == dst);
-      const uint64_t mf = W::ballot(ok && cnt == 0);
+      CommitRec r{};
+      if (ok) r = cm(k);
+      const uint64_t mh = W::ballot(ok && r.cnt > 0 && r.src == src && r.dst == dst);
+      const uint64_t mf = W::ballot(ok && r.cnt == 0);
       if (hit < 0 && mh) hit = k0 + W::ffs(mh);
       if (freeslot < 0 && mf) freeslot = k0 + W::ffs(mf);
     }
     W::sync();
     if (hit >= 0) {
-      if (W::lane() == 0) cc[hit] = (int16_t)(cc[hit] + n);
+      if (W::lane() == 0) cm(hit).cnt = (int16_t)(cm(hit).cnt + n);
     } else if (freeslot >= 0) {
       if (W::lane() == 0) {
-        cs[freeslot] = (int16_t)src;
-        cd[freeslot] = (int16_t)dst;
-        cc[freeslot] = (int16_t)n;
-        co[freeslot] = h.commit_seq;
+        CommitRec& r = cm(freeslot);
+        r.src = (int16_t)src;
+        r.dst = (int16_t)dst;
+        r.cnt = (int16_t)n;
+        r.ord = h.commit_seq;
       }
       h.commit_seq++;
     } else {
@@ -242,12 +252,14 @@ struct Sim {
   }
 
   __device__ __forceinline__ int find_commit(int src, int dst) {
-    const int16_t* cs = H<int16_t>(O.cm_src);
-    const int16_t* cd = H<int16_t>(O.cm_dst);
-    const int16_t* cc = H<int16_t>(O.cm_cnt);
     for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
       const int k = k0 + W::lane();
-      const uint64_t m = W::ballot(k < L.commit_cap && cc[k] > 0 && cs[k] == src && cd[k] == dst);
+      bool hit = false;
+      if (k < L.commit_cap) {
+        const CommitRec r = cm(k);
+        hit = r.cnt > 0 && r.src == src && r.dst == dst;
+      }
+      const uint64_t m = W::ballot(hit);
       if (m) return k0 + W::ffs(m);
     }
     return -1;
@@ -261,10 +273,9 @@ struct Sim {
       fail(SSIM_ERR_INVARIANT);  // ValueError("no commitments from ...") in the reference
       return src;
     }
-    int16_t* cc = H<int16_t>(O.cm_cnt);
-    const int left = cc[k] - 1;
+    const int left = cm(k).cnt - 1;
     W::sync();
-    if (W::lane() == 0) cc[k] = (int16_t)left;
+    if (W::lane() == 0) cm(k).cnt = (int16_t)left;
     W::sync();
     cfrom(src) -= 1;
     check(cfrom(src) >= 0);
@@ -281,16 +292,17 @@ struct Sim {
   }
 
   __device__ __forceinline__ int peek_commitment(int p) {  // :175-180: first key in insertion order, -1 = None
-    const int16_t* cs = H<int16_t>(O.cm_src);
-    const int16_t* cd = H<int16_t>(O.cm_dst);
-    const int16_t* cc = H<int16_t>(O.cm_cnt);
-    const int32_t* co = H<int32_t>(O.cm_ord);
     int best_ord = 0x7FFFFFFF, best_dst = kPoolNone;
     for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
       const int k = k0 + W::lane();
-      const bool ok = k < L.commit_cap && cc[k] > 0 && cs[k] == p;
-      int ord = ok ? co[k] : 0x7FFFFFFF;
-      int dst = ok ? (int)cd[k] : kPoolNone;
+      int ord = 0x7FFFFFFF, dst = kPoolNone;
+      if (k < L.commit_cap) {
+        const CommitRec r = cm(k);
+        if (r.cnt > 0 && r.src == p) {
+          ord = r.ord;
+          dst = r.dst;
+        }
+      }
       W::min_pair(ord, dst);
       if (ord < best_ord) {
         best_ord = ord;
@@ -302,18 +314,19 @@ struct Sim {
 
   // Snapshot of commitments[src] in insertion order into scratch plan: (dst, count) pairs.
   __device__ __forceinline__ int commit_plan(int src, int32_t* plan) {
-    const int16_t* cs = H<int16_t>(O.cm_src);
-    const int16_t* cd = H<int16_t>(O.cm_dst);
-    const int16_t* cc = H<int16_t>(O.cm_cnt);
-    const int32_t* co = H<int32_t>(O.cm_ord);
     int n = 0, last = -1;
     for (;;) {  // selection by increasing insertion stamp (live entries <= N)
       int ord = 0x7FFFFFFF, k_best = -1;
       for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
         const int k = k0 + W::lane();
-        const bool ok = k < L.commit_cap && cc[k] > 0 && cs[k] == src && co[k] > last;
-        int o = ok ? co[k] : 0x7FFFFFFF;
-        int kk = ok ? k : -1;
+        int o = 0x7FFFFFFF, kk = -1;
+        if (k < L.commit_cap) {
+          const CommitRec r = cm(k);
+          if (r.cnt > 0 && r.src == src && r.ord > last) {
+            o = r.ord;
+            kk = k;
+          }
+        }
         W::min_pair(o, kk);
         if (o < ord) {
           ord = o;
@@ -321,7 +334,7 @@ struct Sim {
         }
       }
       if (k_best < 0) break;
-      const int dst = cd[k_best], cnt = cc[k_best];
+      const int dst = cm(k_best).dst, cnt = cm(k_best).cnt;
       W::sync();
       if (W::lane() == 0) {
         plan[2 * n] = dst;
@@ -334,12 +347,15 @@ struct Sim {
     return n;
   }
 
-  // CPython-set tables are staged through LDS: one lane-parallel gather of the table, the serial probe
-  // sequence on LDS, one lane-parallel store back.
+  // CPython-set tables: an 8-slot table lives inline in the PoolRec (LDS-resident with the hot block);
+  // a table that has grown past 8 slots lives in the cold block. Either way an operation stages it into
+  // an LDS scratch table (capacity set_cap, so a resize fits), runs the serial probe sequence there and
+  // writes it back to the home its new size dictates.
+  __device__ __forceinline__ uint8_t* tab_home(int p) const { return pool(p).mask == 7 ? pool(p).tab : ptab(p); }
   __device__ __forceinline__ uint8_t* stage_table(int p) {
     uint8_t* t = S<uint8_t>(O.sc_tab_p);
-    const uint8_t* g = ptab(p);
-    const int size = (int)pmeta(p)->mask + 1;
+    const uint8_t* g = tab_home(p);
+    const int size = (int)pool(p).mask + 1;
     W::sync();
     for (int i = W::lane(); i < size; i += W::kWidth) t[i] = g[i];
     W::sync();
@@ -347,23 +363,27 @@ struct Sim {
   }
   __device__ __forceinline__ void unstage_table(int p, const uint8_t* t) {
     W::sync();
-    uint8_t* g = ptab(p);
-    const int size = (int)pmeta(p)->mask + 1;
+    uint8_t* g = tab_home(p);
+    const int size = (int)pool(p).mask + 1;
     for (int i = W::lane(); i < size; i += W::kWidth) g[i] = t[i];
     W::sync();
   }
   __device__ __forceinline__ void pool_add(int p, int e) {
+    SSIM_TIC(t0);
     uint8_t* t = stage_table(p);
     if (W::lane() == 0) ps_add(pmeta(p), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));
     unstage_table(p, t);
+    SSIM_TOC(t0, kPhPool);
   }
   __device__ __forceinline__ void pool_remove(int p, int e) {
+    SSIM_TIC(t0);
     uint8_t* t = stage_table(p);
     int ok = 1;
     if (W::lane() == 0) ok = ps_remove(pmeta(p), t, (uint32_t)e) ? 1 : 0;
     ok = W::bcast_i(ok, 0);
     unstage_table(p, t);
     check(ok != 0);
+    SSIM_TOC(t0, kPhPool);
   }
 
   __device__ __forceinline__ void move_to_pool(int e, int dst, bool send) {  // :186-220
@@ -392,6 +412,7 @@ struct Sim {
   // Table order of set(e for e in pool.copy() if not busy) — _get_idle_source_executors (:714-728).
   __device__ __forceinline__ int idle_order(int p, int32_t* out) {
     if (p < 0) return 0;
+    SSIM_TIC(t0);
     const uint8_t* t = stage_table(p);
     int n = 0;
     if (W::lane() == 0) {
@@ -406,6 +427,7 @@ struct Sim {
     }
     n = W::bcast_i(n, 0);
     W::sync();
+    SSIM_TOC(t0, kPhPool);
     return n;
   }
 
@@ -433,12 +455,37 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- sampler (tpch.py:75-106, 208-235)
-  __device__ __forceinline__ bool draw(int ts, int wave, int level, double* out) {
-    const int idx = (ts * 3 + wave) * kNumLevels + level;
-    const int len = D.dur_len[idx];
+  // The (wave x exec-level) duration-list descriptors of stage template `ts`: on device one lane-parallel
+  // gather (lane l < 24 holds wave l/8, level l%8) issued together with the key metadata, so a task
+  // launch pays two dependent dataset round trips (descriptors, then the drawn duration).
+  struct DurDesc {
+    int len, off;  // this lane's descriptor (device) — unused by a 1-lane build
+  };
+  __device__ __forceinline__ DurDesc dur_gather(int ts) const {
+    DurDesc d{0, 0};
+    if (W::kWidth >= 24) {
+      const int l = W::lane();
+      if (l < 24) {
+        const int idx = (ts * 3 + (l >> 3)) * kNumLevels + (l & 7);
+        d.len = D.dur_len[idx];
+        d.off = D.dur_off[idx];
+      }
+    }
+    return d;
+  }
+  __device__ __forceinline__ bool draw(int ts, const DurDesc& dd, int wave, int level, double* out) {
+    int len, off;
+    if (W::kWidth >= 24) {
+      len = W::bcast_i(dd.len, wave * 8 + level);
+      off = W::bcast_i(dd.off, wave * 8 + level);
+    } else {
+      const int idx = (ts * 3 + wave) * kNumLevels + level;
+      len = D.dur_len[idx];
+      off = D.dur_off[idx];
+    }
     if (len <= 0) return false;  // KeyError (missing) or ValueError (empty): no RNG consumed
     const uint32_t k = rng.bounded((uint32_t)len);
-    *out = D.durations[D.dur_off[idx] + (int)k];
+    *out = D.durations[off + (int)k];
     return true;
   }
 
@@ -451,6 +498,8 @@ struct Sim {
     const int n_local = job_local(j);
     check(n_local > 0);
     const int ts = st_ts(g);
+    const DurDesc dd = dur_gather(ts);
+    const int keymask = D.ts_fw_keymask[ts], maxlevel = D.ts_fw_maxlevel[ts];
     const double lo = D.intervals[2 * n_local], hi = D.intervals[2 * n_local + 1];
     double key;
     if (lo == hi) {
@@ -460,49 +509,59 @@ struct Sim {
       key = ((double)pt <= (double)n_local - lo) ? lo : hi;
     }
     int level = level_of(key);
-    if (level < 0 || !((D.ts_fw_keymask[ts] >> level) & 1)) level = D.ts_fw_maxlevel[ts];
+    if (level < 0 || !((keymask >> level) & 1)) level = maxlevel;
     double d = 0.0;
     const int last = ex_task(e);
     if (last < 0) {
-      if (draw(ts, 0, level, &d)) return d;
-      if (draw(ts, 1, level, &d)) return d + C.warmup_delay;
+      if (draw(ts, dd, 0, level, &d)) return d;
+      if (draw(ts, dd, 1, level, &d)) return d + C.warmup_delay;
       fail(SSIM_ERR_SAMPLER);
       return 0.0;
     }
     if (last == g - job_base(j)) {
-      if (draw(ts, 2, level, &d)) return d;
+      if (draw(ts, dd, 2, level, &d)) return d;
     }
-    if (draw(ts, 1, level, &d)) return d;
-    if (draw(ts, 0, level, &d)) return d;
+    if (draw(ts, dd, 1, level, &d)) return d;
+    if (draw(ts, dd, 0, level, &d)) return d;
     fail(SSIM_ERR_SAMPLER);
     return 0.0;
   }
 
   // ---------------------------------------------------------------- schedulable-stage search (:505-555)
   __device__ __forceinline__ bool stage_pred(int g, int mode, int jx, int src_job) const {
-    const int j = st_job(g);
+    const StageRec s = stage(g);  // one 16-B record read
+    const int j = s.job;
     if (mode == kScanOnly && j != jx) return false;
     if (mode == kScanExcept && j == jx) return false;
-    if (!(j == src_job || job_supply(j) < L.num_executors)) return false;
-    if (st_sel(g)) return false;
-    if (demand(g) <= 0) return false;
-    const int ts = st_ts(g), base = job_base(j);
-    for (int k = D.ts_parent_base[ts]; k < D.ts_parent_base[ts + 1]; ++k)
-      if (demand(base + D.ts_parents[k]) > 0) return false;
+    const JobRec& jr = job(j);
+    if (!(j == src_job || jr.supply < L.num_executors)) return false;
+    if (s.sel) return false;
+    if (s.rem - (s.mov + s.com) <= 0) return false;
+    const int base = jr.base;
+    for (int k = D.ts_parent_base[s.ts]; k < D.ts_parent_base[s.ts + 1]; ++k) {
+      const StageRec ps = stage(base + D.ts_parents[k]);
+      if (ps.rem - (ps.mov + ps.com) > 0) return false;
+    }
     return true;
   }
 
   // first schedulable stage in node order, or -1
   __device__ __forceinline__ int scan_first(int mode, int jx, int src_job) {
+    SSIM_TIC(t0);
     const int n = h.n_active_stages;
     const int16_t* act = H<int16_t>(O.active_stages);
+    int found = -1;
     for (int i0 = 0; i0 < n; i0 += W::kWidth) {
       const int i = i0 + W::lane();
       const int g = i < n ? act[i] : -1;
       const uint64_t m = W::ballot(g >= 0 && stage_pred(g, mode, jx, src_job));
-      if (m) return W::bcast_i(g, W::ffs(m));
+      if (m) {
+        found = W::bcast_i(g, W::ffs(m));
+        break;
+      }
     }
-    return -1;
+    SSIM_TOC(t0, kPhScan);
+    return found;
   }
   __device__ __forceinline__ bool any_schedulable() { return scan_first(kScanAll, -1, source_job()) >= 0; }
 
@@ -551,7 +610,9 @@ struct Sim {
     st_rem(g) -= 1;
     st_exe(g) += 1;
     if (st_rem(g) == 0) job_sat(j) += 1;
+    SSIM_TIC(t_smp);
     const double dur = task_duration(j, g, e);
+    SSIM_TOC(t_smp, kPhSample);
     ex_task(e) = (int16_t)(g - job_base(j));
     ex_busy(e) = 1;
     st_recent(g) = dur;
@@ -679,7 +740,7 @@ struct Sim {
       const int k = k0 + W::lane();
       if (k <= n) {
         const int p = (k == n) ? job_pool(j) : stage_pool(base + k);
-        ps_init(pmeta(p), ptab(p));
+        ps_init(pmeta(p), pool(p).tab);
         cfrom(p) = 0;
         if (k < n) as[h.n_active_stages + k] = (int16_t)(base + k);
       }
@@ -1164,7 +1225,7 @@ struct Sim {
     }
     for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
       const int k = k0 + W::lane();
-      if (k < L.commit_cap) H<int16_t>(O.cm_cnt)[k] = 0;
+      if (k < L.commit_cap) cm(k) = CommitRec{};
     }
     W::sync();
     {

@@ -1,13 +1,15 @@
-// layout.h — byte layout of the per-env state arena, obs arena and reset staging (see DESIGN.md §Layout).
+// layout.h — byte layout of the per-env state arena, obs arena and reset staging (see DESIGN.md §3).
 // Plain C++ (no HIP), shared by the device library and the test-only host build.
 //
 // Each env owns one block of the state arena = [hot block | cold block]:
-//   hot  — everything the serial event loop touches (header, jobs, compact stage counters, executors,
-//          commitments, pool metadata). Copied into LDS for the duration of a launch when it fits
-//          (hot_bytes + scratch_bytes <= the per-workgroup LDS budget), else used in place in HBM.
-//          Identical offsets in LDS and HBM, so the engine only swaps the base pointer.
-//   cold — HBM only: the CPython-set tables of all pools (staged through LDS per set operation) and
-//          most_recent_duration (read data-parallel by the observation pass).
+//   hot  — everything the serial event loop touches, as fixed-size records (one 16-byte LDS read brings
+//          a whole stage / executor / pool record; ~10 section offsets instead of one per field):
+//          header, JobRec[J], JobTimes[J], active-job list, StageRec[S], active-stage and schedulable
+//          lists, ExecRec[N], selected list, CommitRec[C], PoolRec[P] (set metadata + the 8-slot table
+//          inline). Copied into LDS for the duration of a launch when it fits (`lds_resident`), else
+//          used in place in HBM. Identical offsets in LDS and HBM: the engine only swaps the base.
+//   cold — HBM only: most_recent_duration per stage (read data-parallel by the observation pass) and the
+//          spill area for CPython-set tables that have grown past 8 slots (staged through LDS per use).
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -48,6 +50,52 @@ struct EnvHeader {
 };
 static_assert(sizeof(EnvHeader) % 16 == 0, "header must keep 16-B alignment");
 
+// One stage (env-global index g = job base + local stage id). `done` is derived: rem + exe + done = tasks,
+// so completed <=> rem == 0 && exe == 0.
+struct StageRec {
+  int16_t job, ts;       // owning job, template-stage index into the dataset
+  int16_t rem, exe;      // Stage.num_remaining_tasks / num_executing_tasks (stage.py:5-18)
+  int16_t mov, com;      // ExecutorTracker moving-to / commitments-to this stage
+  int16_t unmet;         // parents not yet completed (frontier <=> unmet == 0, job.py:93-128)
+  uint8_t sel, pad;      // selected in the current round (spark_sched_sim.py:304)
+};
+static_assert(sizeof(StageRec) == 16, "stage record");
+
+struct JobRec {
+  int16_t tpl, base, nst, nact;      // template, first env stage, #stages, #active stages
+  int16_t sat, local, supply, state; // saturated count, |local_executors|, exec supply, 0/1/2
+  int32_t arr_dec, done_dec;         // decision counter at arrival / completion (reward union)
+  int32_t pad[2];
+};
+static_assert(sizeof(JobRec) == 32, "job record");
+
+struct JobTimes {
+  double tarr, tdone;  // Job.t_arrival / t_completed
+};
+
+struct ExecRec {
+  int16_t loc, job, task, busy;     // pool code, job (-1 None), last task's local stage (-1 None), executing
+  int16_t ev_type, ev_stage;        // pending event (at most one per executor)
+  int32_t ev_seq;                   // -1 = no pending event
+  double ev_t;
+  int64_t pad;
+};
+static_assert(sizeof(ExecRec) == 32, "executor record");
+
+struct CommitRec {
+  int16_t src, dst, cnt, pad;  // ExecutorTracker._commitments[src][dst] = cnt (deleted at 0)
+  int32_t ord, pad2;           // dict insertion order stamp
+};
+static_assert(sizeof(CommitRec) == 16, "commitment record");
+
+// CPython set of one pool: metadata + the table while it has 8 slots (bigger tables spill to the cold block)
+struct PoolRec {
+  uint16_t mask, fill, used;  // PySetMeta layout (pyset.h)
+  int16_t cfrom;              // ExecutorTracker._num_commitments_from[pool]
+  uint8_t tab[8];
+};
+static_assert(sizeof(PoolRec) == 16, "pool record");
+
 constexpr int kNumLevels = 8;  // EXEC_LEVELS (tpch.py:238)
 constexpr int kTraceBytes = 32;
 constexpr int64_t kResetHeadBytes = 64;  // ssim_reset_record padded
@@ -65,28 +113,17 @@ struct TraceRec {  // one popped event
 };
 static_assert(sizeof(TraceRec) == kTraceBytes, "trace record size");
 
-// Field offsets. hot/cold offsets are relative to the start of the hot/cold block; sc_* to the scratch.
+// Section offsets. hot/cold offsets are relative to the start of the hot/cold block; sc_* to the scratch.
 struct StateOffsets {
-  int64_t hot_bytes, cold_bytes, lds_bytes;  // lds_bytes = hot + scratch when LDS-resident, else scratch
+  int64_t hot_bytes, cold_bytes, lds_bytes;  // lds_bytes = scratch (+ hot when LDS-resident)
   int32_t lds_resident, pad;
-  // hot: header, jobs (int16 unless noted), stages (int16), executors, commitments, pools
-  int64_t hdr;
-  int64_t job_tpl, job_base, job_nst, job_nact, job_sat, job_local, job_supply, job_state;
-  int64_t job_arr_dec, job_done_dec;  // int32
-  int64_t job_tarr, job_tdone;        // float64
-  int64_t active_jobs;
-  int64_t st_job, st_ts, st_rem, st_exe, st_mov, st_com, st_unmet, st_sel /*uint8*/, active_stages, sched_list;
-  int64_t ex_loc, ex_job, ex_task, ex_busy, ev_type, ev_stage; /*int16*/
-  int64_t ev_seq /*int32*/, ev_t /*float64*/, sel_list;
-  int64_t cm_src, cm_dst, cm_cnt /*int16*/, cm_ord /*int32*/;
-  int64_t pool_meta /*PySetMeta*/, pool_cfrom /*int16*/;
-  // cold
-  int64_t st_recent /*float64*/, pool_tab /*uint8 [P][set_cap]*/;
-  // scratch (LDS)
-  int64_t sc_row_of /*int16*/, sc_keys_a, sc_keys_b /*int32*/, sc_plan /*int32*/, sc_tab_a, sc_tab_b, sc_tab_p;
+  int64_t hdr, jobs, jtimes, active_jobs, stages, active_stages, sched_list, execs, sel_list, commits, pools;
+  int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/;
+  int64_t sc_row_of /*int16[S]*/, sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b,
+      sc_tab_p /*uint8[set_cap]*/;
 };
 
-inline int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
+constexpr int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
 
 inline int set_cap_for(int n) {  // smallest power of two > 4N (max CPython set table for N keys)
   int c = 8;
@@ -122,44 +159,16 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
     return r;
   };
   O->hdr = take(sizeof(EnvHeader));
-  O->job_tpl = take(2 * J);
-  O->job_base = take(2 * J);
-  O->job_nst = take(2 * J);
-  O->job_nact = take(2 * J);
-  O->job_sat = take(2 * J);
-  O->job_local = take(2 * J);
-  O->job_supply = take(2 * J);
-  O->job_state = take(2 * J);
+  O->jobs = take((int64_t)sizeof(JobRec) * J);
+  O->jtimes = take((int64_t)sizeof(JobTimes) * J);
   O->active_jobs = take(2 * J);
-  O->job_arr_dec = take(4 * J);
-  O->job_done_dec = take(4 * J);
-  O->job_tarr = take(8 * J);
-  O->job_tdone = take(8 * J);
-  O->st_job = take(2 * S);
-  O->st_ts = take(2 * S);
-  O->st_rem = take(2 * S);
-  O->st_exe = take(2 * S);
-  O->st_mov = take(2 * S);
-  O->st_com = take(2 * S);
-  O->st_unmet = take(2 * S);
-  O->st_sel = take(S);
+  O->stages = take((int64_t)sizeof(StageRec) * S);
   O->active_stages = take(2 * S);
   O->sched_list = take(2 * S);
-  O->ex_loc = take(2 * N);
-  O->ex_job = take(2 * N);
-  O->ex_task = take(2 * N);
-  O->ex_busy = take(2 * N);
-  O->ev_type = take(2 * N);
-  O->ev_stage = take(2 * N);
-  O->ev_seq = take(4 * N);
-  O->ev_t = take(8 * N);
+  O->execs = take((int64_t)sizeof(ExecRec) * N);
   O->sel_list = take(2 * (N + 1));
-  O->cm_src = take(2 * C);
-  O->cm_dst = take(2 * C);
-  O->cm_cnt = take(2 * C);
-  O->cm_ord = take(4 * C);
-  O->pool_meta = take(6 * P);
-  O->pool_cfrom = take(2 * P);
+  O->commits = take((int64_t)sizeof(CommitRec) * C);
+  O->pools = take((int64_t)sizeof(PoolRec) * P);
   O->hot_bytes = align16(o);
 
   int64_t c = 0;

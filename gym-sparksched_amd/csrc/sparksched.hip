@@ -28,7 +28,14 @@ struct WaveHip {
   __device__ static __forceinline__ int rank(uint64_t m) {  // set bits of m below this lane
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   }
-  __device__ static __forceinline__ int bcast_i(int v, int l) { return __shfl(v, l); }
+  // v_readlane (VALU -> SGPR) instead of an LDS-path ds_bpermute; `l` is wave-uniform
+  __device__ static __forceinline__ int bcast_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+  __device__ static __forceinline__ double bcast_d(double v, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+  }
   __device__ static __forceinline__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -50,29 +57,43 @@ struct WaveHip {
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
     return x;
   }
-  // lexicographic min of (key, val) across the wave, result in every lane
+  // Sparse argmins: the candidates are few (live commitments, pending executor events), so walk the
+  // ballot of valid lanes with v_readlane instead of a 6-round ds_bpermute butterfly.
+  // lexicographic min of (key, val) over lanes with key != INT_MAX; result in every lane
   __device__ static __forceinline__ void min_pair(int& key, int& val) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const int k2 = __shfl_xor(key, off), v2 = __shfl_xor(val, off);
-      if (k2 < key || (k2 == key && v2 < val)) {
-        key = k2;
-        val = v2;
+    uint64_t m = ballot(key != 0x7FFFFFFF);
+    int bk = 0x7FFFFFFF, bv = val;
+    while (m) {
+      const int l = ffs(m);
+      m &= m - 1;
+      const int k2 = bcast_i(key, l), v2 = bcast_i(val, l);
+      if (k2 < bk || (k2 == bk && v2 < bv)) {
+        bk = k2;
+        bv = v2;
       }
     }
+    key = bk;
+    val = bv;
   }
-  // min of (t, seq) with payload idx across the wave
+  // min of (t, seq) with payload idx over lanes with idx >= 0; result in every lane
   __device__ static __forceinline__ void min_event(double& t, int& seq, int& idx) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double t2 = __shfl_xor(t, off);
-      const int s2 = __shfl_xor(seq, off), i2 = __shfl_xor(idx, off);
-      if (t2 < t || (t2 == t && s2 < seq)) {
-        t = t2;
-        seq = s2;
-        idx = i2;
+    uint64_t m = ballot(idx >= 0);
+    double bt = t;
+    int bs = 0x7FFFFFFF, bi = -1;
+    while (m) {
+      const int l = ffs(m);
+      m &= m - 1;
+      const double t2 = bcast_d(t, l);
+      const int s2 = bcast_i(seq, l);
+      if (bi < 0 || t2 < bt || (t2 == bt && s2 < bs)) {
+        bt = t2;
+        bs = s2;
+        bi = bcast_i(idx, l);
       }
     }
+    t = bt;
+    seq = bs;
+    idx = bi;
   }
 };
 
@@ -153,13 +174,19 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
 #endif
 }
 
-// job state (int16 in the hot block) -> int32 [num_envs][job_cap]
-__global__ __launch_bounds__(64) void k_job_state(const Params* __restrict__ P, const uint8_t* state,
-                                                  int32_t* out) {
+// per-job arrival/completion times and state (JobRec/JobTimes in the hot block) -> [num_envs][job_cap]
+__global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, const uint8_t* state,
+                                                  double* ta, double* tc, int32_t* st) {
   const int eid = blockIdx.x, J = P->L.job_cap;
-  const int16_t* js =
-      reinterpret_cast<const int16_t*>(state + kParamsReserve + (int64_t)eid * P->L.env_bytes + P->O.job_state);
-  for (int j = threadIdx.x; j < J; j += 64) out[(int64_t)eid * J + j] = js[j];
+  const uint8_t* hot = state + kParamsReserve + (int64_t)eid * P->L.env_bytes;
+  const JobRec* jr = reinterpret_cast<const JobRec*>(hot + P->O.jobs);
+  const JobTimes* jt = reinterpret_cast<const JobTimes*>(hot + P->O.jtimes);
+  for (int j = threadIdx.x; j < J; j += 64) {
+    const int64_t o = (int64_t)eid * J + j;
+    if (ta) ta[o] = jt[j].tarr;
+    if (tc) tc[o] = jt[j].tdone;
+    if (st) st[o] = jr[j].state;
+  }
 }
 
 // ------------------------------------------------------------------------------------------ C ABI
@@ -287,23 +314,9 @@ extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed
 
 extern "C" int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32_t* state, void* stream) {
   if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_job_times: null handle");
-  const ssim_layout& L = h->params.L;
-  const StateOffsets& O = h->params.O;
-  const size_t J = (size_t)L.job_cap, B = (size_t)L.num_envs, pitch = (size_t)L.env_bytes;
-  const uint8_t* base = h->state + kParamsReserve;
-  hipStream_t s = (hipStream_t)stream;
-  int rc = SSIM_OK;
-  if (t_arrival)
-    rc = hip_check(hipMemcpy2DAsync(t_arrival, J * 8, base + O.job_tarr, pitch, J * 8, B, hipMemcpyDeviceToDevice, s),
-                   "job t_arrival copy");
-  if (rc == SSIM_OK && t_completed)
-    rc = hip_check(hipMemcpy2DAsync(t_completed, J * 8, base + O.job_tdone, pitch, J * 8, B, hipMemcpyDeviceToDevice, s),
-                   "job t_completed copy");
-  if (rc == SSIM_OK && state) {
-    hipLaunchKernelGGL(k_job_state, dim3(L.num_envs), dim3(64), 0, s, dparams(h), h->state, state);
-    rc = hip_check(hipGetLastError(), "k_job_state launch");
-  }
-  return rc;
+  hipLaunchKernelGGL(k_job_times, dim3(h->params.L.num_envs), dim3(64), 0, (hipStream_t)stream, dparams(h), h->state,
+                     t_arrival, t_completed, state);
+  return hip_check(hipGetLastError(), "k_job_times launch");
 }
 
 extern "C" const char* ssim_last_error(void) { return g_err; }

@@ -14,7 +14,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "gym-sparksched_amd"))
 
-PHASES = ["policy", "action", "round_check", "fulfill", "pop", "handle", "post_scan", "observe"]
+PHASES = ["policy", "action", "round_check", "fulfill", "pop", "handle", "post_scan", "observe",
+          "(sample)", "(pool ops)", "(scans)", "(hot load/save)"]
+TOP = 8  # the first TOP phases are disjoint; the rest are inclusive sub-timers
 
 
 def build_prof():
@@ -74,8 +76,9 @@ def main():
     dec = d1 - d0
     tot = p.sum(axis=0)
     print(f"decisions {dec}, events {e1 - e0} ({(e1 - e0) / dec:.2f}/decision)")
+    top = tot[:TOP].sum()
     for name, v in zip(PHASES, tot):
-        print(f"  {name:12s} {v / dec:10.1f} ticks/decision  {100 * v / tot.sum():5.1f}%")
+        print(f"  {name:16s} {v / dec:10.1f} cycles/decision  {100 * v / top:5.1f}%")
     res["phases_ticks_per_decision"] = {n: float(v / dec) for n, v in zip(PHASES, tot)}
     res["events_per_decision"] = (e1 - e0) / dec
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)

@@ -137,11 +137,14 @@ void hs_job_times(hs_handle* h, double* ta, double* tc, int32_t* st) {
   const Params* P = h->params;
   const int J = P->L.job_cap;
   for (int e = 0; e < P->L.num_envs; ++e) {
-    const uint8_t* env = h->state + kParamsReserve + (int64_t)e * P->L.env_bytes;
-    memcpy(ta + (int64_t)e * J, env + P->O.job_tarr, 8 * (size_t)J);
-    memcpy(tc + (int64_t)e * J, env + P->O.job_tdone, 8 * (size_t)J);
-    const int16_t* js = reinterpret_cast<const int16_t*>(env + P->O.job_state);
-    for (int j = 0; j < J; ++j) st[(int64_t)e * J + j] = js[j];
+    const uint8_t* hot = h->state + kParamsReserve + (int64_t)e * P->L.env_bytes;
+    const JobRec* jr = reinterpret_cast<const JobRec*>(hot + P->O.jobs);
+    const JobTimes* jt = reinterpret_cast<const JobTimes*>(hot + P->O.jtimes);
+    for (int j = 0; j < J; ++j) {
+      ta[(int64_t)e * J + j] = jt[j].tarr;
+      tc[(int64_t)e * J + j] = jt[j].tdone;
+      st[(int64_t)e * J + j] = jr[j].state;
+    }
   }
 }
 
