@@ -34,6 +34,18 @@
 
 namespace ssim {
 
+// Dataset pointers are loaded from the Params block, so the compiler sees generic pointers and would emit
+// FLAT loads; the cast to the global address space turns them into global_load (test host build: no-op).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SSIM_GLOBAL __attribute__((address_space(1)))
+#else
+#define SSIM_GLOBAL
+#endif
+template <class T>
+__device__ __forceinline__ T ldg(const T* p, int64_t i) {
+  return ((const SSIM_GLOBAL T*)p)[i];
+}
+
 // top-level phases (disjoint) then inclusive sub-timers (nested inside the top-level ones)
 enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kPhHandle, kPhPostScan, kPhObserve,
                  kPhSample, kPhPool, kPhScan, kPhLoadSave, kNumPhases };
@@ -57,12 +69,15 @@ struct Params {
 constexpr int64_t kParamsReserve = 4096;
 static_assert(sizeof(Params) <= kParamsReserve, "params block");
 
-template <class W>
+// kN / kJ: executor count and job cap as compile-time constants (0 = read from the layout at run time).
+// A specialised instantiation sees every (N, J)-dependent offset, loop bound and table size as a constant.
+template <class W, int kN = 0, int kJ = 0>
 struct Sim {
   const ssim_layout& L;
-  const StateOffsets& O;
   const ssim_dataset& D;
   const ssim_config& C;
+  const int32_t NE, JC, SC;  // executors, job cap, stage cap
+  const StateOffsets O;      // re-derived from (NE, JC, SC): same function as the host layout
   uint8_t* ghot;  // this env's hot block in HBM
   uint8_t* hot;   // working copy of the hot block (LDS when resident, else == ghot)
   uint8_t* cold;  // this env's cold block in HBM
@@ -75,14 +90,15 @@ struct Sim {
   uint64_t prof[kNumPhases] = {0};
 #endif
 
-  // `lds` = this wave's LDS block: [scratch | hot copy (if resident)]; resident=false keeps hot in HBM.
+  // `lds` = this wave's LDS block: [hot copy (if resident) | scratch]; resident=false keeps hot in HBM.
   __device__ __forceinline__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* lds,
                                  uint8_t* obs_arena, int32_t env_index, bool resident)
-      : L(p->L), O(p->O), D(p->D), C(p->C),
-        ghot(state_arena + kParamsReserve + (int64_t)env_index * p->L.env_bytes),
-        hot(resident ? lds + p->L.scratch_bytes : state_arena + kParamsReserve + (int64_t)env_index * p->L.env_bytes),
-        cold(state_arena + kParamsReserve + (int64_t)env_index * p->L.env_bytes + p->O.hot_bytes), scr(lds),
-        obs(obs_arena), eid(env_index) {}
+      : L(p->L), D(p->D), C(p->C), NE(kN ? kN : p->L.num_executors), JC(kJ ? kJ : p->L.job_cap),
+        SC(p->L.stage_cap), O(state_offsets(NE, JC, SC)),
+        ghot(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
+        hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
+        cold(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes + O.hot_bytes),
+        scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index) {}
 
   // ---------------------------------------------------------------- hot-block residency
   __device__ __forceinline__ void copy16(uint8_t* dst, const uint8_t* src, int64_t bytes) {
@@ -113,7 +129,10 @@ struct Sim {
     return reinterpret_cast<T*>(scr + off);
   }
   __device__ __forceinline__ void load_header() {
-    h = *H<EnvHeader>(O.hdr);
+    uint32_t w[sizeof(EnvHeader) / 4];  // wave-uniform copy: the header lives in SGPRs
+    __builtin_memcpy(w, H<EnvHeader>(O.hdr), sizeof(w));
+    for (int i = 0; i < (int)(sizeof(EnvHeader) / 4); ++i) w[i] = W::uni(w[i]);
+    __builtin_memcpy(&h, w, sizeof(w));
     rng.s_hi = h.rng_s_hi;
     rng.s_lo = h.rng_s_lo;
     rng.i_hi = h.rng_i_hi;
@@ -138,60 +157,92 @@ struct Sim {
     if (!ok) h.err |= SSIM_ERR_INVARIANT;
   }
 
-  // records (layout.h); accessors keep the algorithm code independent of the record packing
+  // Field access. Two kinds, by who is asking:
+  //  * serial code (wave-uniform index): the named accessors below return a UF proxy whose reads go
+  //    through W::uni, so the value lands in an SGPR and the code that uses it is scalar;
+  //  * lane-parallel loops (index differs per lane): read whole records by value (stage(g), job(j),
+  //    exr(e) ...) — never through UF, whose readfirstlane would broadcast lane 0's value.
+  template <class T>
+  struct UF {
+    T* p;
+    __device__ __forceinline__ operator T() const { return W::uni(*p); }
+    __device__ __forceinline__ UF& operator=(T v) {
+      *p = v;
+      return *this;
+    }
+    __device__ __forceinline__ UF& operator+=(int v) {
+      *p = (T)(*p + v);
+      return *this;
+    }
+    __device__ __forceinline__ UF& operator-=(int v) {
+      *p = (T)(*p - v);
+      return *this;
+    }
+  };
+  template <class T>
+  __device__ __forceinline__ T ld(const T* q) const {  // uniform read of a scratch / list entry
+    return W::uni(*q);
+  }
+  template <class T>
+  __device__ __forceinline__ T ldu(const T* q, int64_t i) const {  // uniform dataset read
+    return W::uni(ldg(q, i));
+  }
+
+  // records (layout.h)
   __device__ __forceinline__ StageRec& stage(int g) const { return H<StageRec>(O.stages)[g]; }
   __device__ __forceinline__ JobRec& job(int j) const { return H<JobRec>(O.jobs)[j]; }
   __device__ __forceinline__ JobTimes& jtimes(int j) const { return H<JobTimes>(O.jtimes)[j]; }
   __device__ __forceinline__ ExecRec& exr(int e) const { return H<ExecRec>(O.execs)[e]; }
   __device__ __forceinline__ CommitRec& cm(int k) const { return H<CommitRec>(O.commits)[k]; }
   __device__ __forceinline__ PoolRec& pool(int p) const { return H<PoolRec>(O.pools)[p]; }
+  __device__ __forceinline__ double* recent() const { return reinterpret_cast<double*>(cold + O.st_recent); }
   // stages (env-global index g = job base + local stage id); `done` is derived: rem + exe + done = tasks
-  __device__ __forceinline__ int16_t& st_job(int g) const { return stage(g).job; }
-  __device__ __forceinline__ int16_t& st_ts(int g) const { return stage(g).ts; }
-  __device__ __forceinline__ int16_t& st_rem(int g) const { return stage(g).rem; }
-  __device__ __forceinline__ int16_t& st_exe(int g) const { return stage(g).exe; }
-  __device__ __forceinline__ int16_t& st_mov(int g) const { return stage(g).mov; }
-  __device__ __forceinline__ int16_t& st_com(int g) const { return stage(g).com; }
-  __device__ __forceinline__ int16_t& st_unmet(int g) const { return stage(g).unmet; }
-  __device__ __forceinline__ uint8_t& st_sel(int g) const { return stage(g).sel; }
-  __device__ __forceinline__ double& st_recent(int g) const { return reinterpret_cast<double*>(cold + O.st_recent)[g]; }
+  __device__ __forceinline__ UF<int16_t> st_job(int g) const { return {&stage(g).job}; }
+  __device__ __forceinline__ UF<int16_t> st_ts(int g) const { return {&stage(g).ts}; }
+  __device__ __forceinline__ UF<int16_t> st_rem(int g) const { return {&stage(g).rem}; }
+  __device__ __forceinline__ UF<int16_t> st_exe(int g) const { return {&stage(g).exe}; }
+  __device__ __forceinline__ UF<int16_t> st_mov(int g) const { return {&stage(g).mov}; }
+  __device__ __forceinline__ UF<int16_t> st_com(int g) const { return {&stage(g).com}; }
+  __device__ __forceinline__ UF<int16_t> st_unmet(int g) const { return {&stage(g).unmet}; }
+  __device__ __forceinline__ UF<uint8_t> st_sel(int g) const { return {&stage(g).sel}; }
+  __device__ __forceinline__ UF<double> st_recent(int g) const { return {recent() + g}; }
   __device__ __forceinline__ bool st_completed(int g) const { return st_rem(g) == 0 && st_exe(g) == 0; }
   // jobs
-  __device__ __forceinline__ int16_t& job_tpl(int j) const { return job(j).tpl; }
-  __device__ __forceinline__ int16_t& job_base(int j) const { return job(j).base; }
-  __device__ __forceinline__ int16_t& job_nst(int j) const { return job(j).nst; }
-  __device__ __forceinline__ int16_t& job_nact(int j) const { return job(j).nact; }
-  __device__ __forceinline__ int16_t& job_sat(int j) const { return job(j).sat; }
-  __device__ __forceinline__ int16_t& job_local(int j) const { return job(j).local; }
-  __device__ __forceinline__ int16_t& job_supply(int j) const { return job(j).supply; }
-  __device__ __forceinline__ int16_t& job_state(int j) const { return job(j).state; }
-  __device__ __forceinline__ int32_t& job_arr_dec(int j) const { return job(j).arr_dec; }
-  __device__ __forceinline__ int32_t& job_done_dec(int j) const { return job(j).done_dec; }
-  __device__ __forceinline__ double& job_tarr(int j) const { return jtimes(j).tarr; }
-  __device__ __forceinline__ double& job_tdone(int j) const { return jtimes(j).tdone; }
+  __device__ __forceinline__ UF<int16_t> job_tpl(int j) const { return {&job(j).tpl}; }
+  __device__ __forceinline__ UF<int16_t> job_base(int j) const { return {&job(j).base}; }
+  __device__ __forceinline__ UF<int16_t> job_nst(int j) const { return {&job(j).nst}; }
+  __device__ __forceinline__ UF<int16_t> job_nact(int j) const { return {&job(j).nact}; }
+  __device__ __forceinline__ UF<int16_t> job_sat(int j) const { return {&job(j).sat}; }
+  __device__ __forceinline__ UF<int16_t> job_local(int j) const { return {&job(j).local}; }
+  __device__ __forceinline__ UF<int16_t> job_supply(int j) const { return {&job(j).supply}; }
+  __device__ __forceinline__ UF<int16_t> job_state(int j) const { return {&job(j).state}; }
+  __device__ __forceinline__ UF<int32_t> job_arr_dec(int j) const { return {&job(j).arr_dec}; }
+  __device__ __forceinline__ UF<int32_t> job_done_dec(int j) const { return {&job(j).done_dec}; }
+  __device__ __forceinline__ UF<double> job_tarr(int j) const { return {&jtimes(j).tarr}; }
+  __device__ __forceinline__ UF<double> job_tdone(int j) const { return {&jtimes(j).tdone}; }
   // executors
-  __device__ __forceinline__ int16_t& ex_loc(int e) const { return exr(e).loc; }
-  __device__ __forceinline__ int16_t& ex_job(int e) const { return exr(e).job; }
-  __device__ __forceinline__ int16_t& ex_task(int e) const { return exr(e).task; }
-  __device__ __forceinline__ int16_t& ex_busy(int e) const { return exr(e).busy; }
-  __device__ __forceinline__ double& ev_t(int e) const { return exr(e).ev_t; }
-  __device__ __forceinline__ int32_t& ev_seq(int e) const { return exr(e).ev_seq; }
-  __device__ __forceinline__ int16_t& ev_type(int e) const { return exr(e).ev_type; }
-  __device__ __forceinline__ int16_t& ev_stage(int e) const { return exr(e).ev_stage; }
+  __device__ __forceinline__ UF<int16_t> ex_loc(int e) const { return {&exr(e).loc}; }
+  __device__ __forceinline__ UF<int16_t> ex_job(int e) const { return {&exr(e).job}; }
+  __device__ __forceinline__ UF<int16_t> ex_task(int e) const { return {&exr(e).task}; }
+  __device__ __forceinline__ UF<int16_t> ex_busy(int e) const { return {&exr(e).busy}; }
+  __device__ __forceinline__ UF<double> ev_t(int e) const { return {&exr(e).ev_t}; }
+  __device__ __forceinline__ UF<int32_t> ev_seq(int e) const { return {&exr(e).ev_seq}; }
+  __device__ __forceinline__ UF<int16_t> ev_type(int e) const { return {&exr(e).ev_type}; }
+  __device__ __forceinline__ UF<int16_t> ev_stage(int e) const { return {&exr(e).ev_stage}; }
   // pools: code 0 = COMMON, 1+j = job j, 1+job_cap+g = stage g, -1 = None
   __device__ __forceinline__ int32_t job_pool(int j) const { return 1 + j; }
-  __device__ __forceinline__ int32_t stage_pool(int g) const { return 1 + L.job_cap + g; }
-  __device__ __forceinline__ bool is_stage_pool(int p) const { return p > L.job_cap; }
-  __device__ __forceinline__ int32_t pool_stage(int p) const { return p - 1 - L.job_cap; }
+  __device__ __forceinline__ int32_t stage_pool(int g) const { return 1 + JC + g; }
+  __device__ __forceinline__ bool is_stage_pool(int p) const { return p > JC; }
+  __device__ __forceinline__ int32_t pool_stage(int p) const { return p - 1 - JC; }
   __device__ __forceinline__ int32_t pool_job(int p) const {  // pool_key[0]; -1 = None
     if (p <= 0) return -1;
-    if (p <= L.job_cap) return p - 1;
-    return st_job(p - 1 - L.job_cap);
+    if (p <= JC) return p - 1;
+    return st_job(p - 1 - JC);
   }
   __device__ __forceinline__ PySetMeta* pmeta(int p) const { return reinterpret_cast<PySetMeta*>(&pool(p)); }
-  __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + O.pool_tab + (int64_t)p * L.set_cap; }
-  __device__ __forceinline__ int16_t& cfrom(int p) const { return pool(p).cfrom; }
-  __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)pool(p).used; }
+  __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + O.pool_tab + (int64_t)p * set_cap_for(NE); }
+  __device__ __forceinline__ UF<int16_t> cfrom(int p) const { return {&pool(p).cfrom}; }
+  __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)W::uni(pool(p).used); }
 
   // ---------------------------------------------------------------- tracker (executor_tracker.py)
   __device__ __forceinline__ int32_t source_job() const {  // :98-102
@@ -217,9 +268,9 @@ struct Sim {
     check(src >= 0);
     if (src < 0) return;
     int hit = -1, freeslot = -1;
-    for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+    for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
       const int k = k0 + W::lane();
-      const bool ok = k < L.commit_cap;
+      const bool ok = k < commit_cap_for(NE);
       CommitRec r{};
       if (ok) r = cm(k);
       const uint64_t mh = W::ballot(ok && r.cnt > 0 && r.src == src && r.dst == dst);
@@ -252,10 +303,10 @@ struct Sim {
   }
 
   __device__ __forceinline__ int find_commit(int src, int dst) {
-    for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+    for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
       const int k = k0 + W::lane();
       bool hit = false;
-      if (k < L.commit_cap) {
+      if (k < commit_cap_for(NE)) {
         const CommitRec r = cm(k);
         hit = r.cnt > 0 && r.src == src && r.dst == dst;
       }
@@ -293,10 +344,10 @@ struct Sim {
 
   __device__ __forceinline__ int peek_commitment(int p) {  // :175-180: first key in insertion order, -1 = None
     int best_ord = 0x7FFFFFFF, best_dst = kPoolNone;
-    for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+    for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
       const int k = k0 + W::lane();
       int ord = 0x7FFFFFFF, dst = kPoolNone;
-      if (k < L.commit_cap) {
+      if (k < commit_cap_for(NE)) {
         const CommitRec r = cm(k);
         if (r.cnt > 0 && r.src == p) {
           ord = r.ord;
@@ -317,10 +368,10 @@ struct Sim {
     int n = 0, last = -1;
     for (;;) {  // selection by increasing insertion stamp (live entries <= N)
       int ord = 0x7FFFFFFF, k_best = -1;
-      for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+      for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
         const int k = k0 + W::lane();
         int o = 0x7FFFFFFF, kk = -1;
-        if (k < L.commit_cap) {
+        if (k < commit_cap_for(NE)) {
           const CommitRec r = cm(k);
           if (r.cnt > 0 && r.src == src && r.ord > last) {
             o = r.ord;
@@ -351,36 +402,45 @@ struct Sim {
   // a table that has grown past 8 slots lives in the cold block. Either way an operation stages it into
   // an LDS scratch table (capacity set_cap, so a resize fits), runs the serial probe sequence there and
   // writes it back to the home its new size dictates.
-  __device__ __forceinline__ uint8_t* tab_home(int p) const { return pool(p).mask == 7 ? pool(p).tab : ptab(p); }
+  // The two homes are separate branches (not one selected pointer) so each copy compiles to ds_* or
+  // global_* instructions rather than FLAT.
   __device__ __forceinline__ uint8_t* stage_table(int p) {
     uint8_t* t = S<uint8_t>(O.sc_tab_p);
-    const uint8_t* g = tab_home(p);
-    const int size = (int)pool(p).mask + 1;
+    const int size = (int)W::uni(pool(p).mask) + 1;
     W::sync();
-    for (int i = W::lane(); i < size; i += W::kWidth) t[i] = g[i];
+    if (size == 8) {
+      const uint8_t* g = pool(p).tab;
+      for (int i = W::lane(); i < 8; i += W::kWidth) t[i] = g[i];
+    } else {
+      const uint8_t* g = ptab(p);
+      for (int i = W::lane(); i < size; i += W::kWidth) t[i] = g[i];
+    }
     W::sync();
     return t;
   }
   __device__ __forceinline__ void unstage_table(int p, const uint8_t* t) {
     W::sync();
-    uint8_t* g = tab_home(p);
-    const int size = (int)pool(p).mask + 1;
-    for (int i = W::lane(); i < size; i += W::kWidth) g[i] = t[i];
+    const int size = (int)W::uni(pool(p).mask) + 1;
+    if (size == 8) {
+      uint8_t* g = pool(p).tab;
+      for (int i = W::lane(); i < 8; i += W::kWidth) g[i] = t[i];
+    } else {
+      uint8_t* g = ptab(p);
+      for (int i = W::lane(); i < size; i += W::kWidth) g[i] = t[i];
+    }
     W::sync();
   }
   __device__ __forceinline__ void pool_add(int p, int e) {
     SSIM_TIC(t0);
     uint8_t* t = stage_table(p);
-    if (W::lane() == 0) ps_add(pmeta(p), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));
+    ps_add<W>(pmeta(p), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));
     unstage_table(p, t);
     SSIM_TOC(t0, kPhPool);
   }
   __device__ __forceinline__ void pool_remove(int p, int e) {
     SSIM_TIC(t0);
     uint8_t* t = stage_table(p);
-    int ok = 1;
-    if (W::lane() == 0) ok = ps_remove(pmeta(p), t, (uint32_t)e) ? 1 : 0;
-    ok = W::bcast_i(ok, 0);
+    const bool ok = ps_remove<W>(pmeta(p), t, (uint32_t)e);
     unstage_table(p, t);
     check(ok != 0);
     SSIM_TOC(t0, kPhPool);
@@ -414,18 +474,16 @@ struct Sim {
     if (p < 0) return 0;
     SSIM_TIC(t0);
     const uint8_t* t = stage_table(p);
-    int n = 0;
-    if (W::lane() == 0) {
-      const PySetMeta* m = pmeta(p);
-      n = ps_keys(m, t, out);
-      ps_copy_order(m, out, n, S<uint8_t>(O.sc_tab_a));
-      int k = 0;
-      for (int i = 0; i < n; ++i)
-        if (!ex_busy(out[i])) out[k++] = out[i];
-      n = k;
-      ps_build_order(out, n, S<uint8_t>(O.sc_tab_b), S<int32_t>(O.sc_keys_b));
+    const PySetMeta* m = pmeta(p);
+    int n = ps_keys<W>(m, t, out);
+    ps_copy_order<W>(m, out, n, S<uint8_t>(O.sc_tab_a));
+    int k = 0;
+    for (int i = 0; i < n; ++i) {
+      const int e = ld(out + i);
+      if (!ex_busy(e)) out[k++] = e;
     }
-    n = W::bcast_i(n, 0);
+    n = k;
+    ps_build_order<W>(out, n, S<uint8_t>(O.sc_tab_b), S<int32_t>(O.sc_keys_b));
     W::sync();
     SSIM_TOC(t0, kPhPool);
     return n;
@@ -467,8 +525,8 @@ struct Sim {
       const int l = W::lane();
       if (l < 24) {
         const int idx = (ts * 3 + (l >> 3)) * kNumLevels + (l & 7);
-        d.len = D.dur_len[idx];
-        d.off = D.dur_off[idx];
+        d.len = ldg(D.dur_len, idx);
+        d.off = ldg(D.dur_off, idx);
       }
     }
     return d;
@@ -480,12 +538,12 @@ struct Sim {
       off = W::bcast_i(dd.off, wave * 8 + level);
     } else {
       const int idx = (ts * 3 + wave) * kNumLevels + level;
-      len = D.dur_len[idx];
-      off = D.dur_off[idx];
+      len = ldu(D.dur_len, idx);
+      off = ldu(D.dur_off, idx);
     }
     if (len <= 0) return false;  // KeyError (missing) or ValueError (empty): no RNG consumed
     const uint32_t k = rng.bounded((uint32_t)len);
-    *out = D.durations[off + (int)k];
+    *out = ldu(D.durations, off + (int)k);
     return true;
   }
 
@@ -499,8 +557,8 @@ struct Sim {
     check(n_local > 0);
     const int ts = st_ts(g);
     const DurDesc dd = dur_gather(ts);
-    const int keymask = D.ts_fw_keymask[ts], maxlevel = D.ts_fw_maxlevel[ts];
-    const double lo = D.intervals[2 * n_local], hi = D.intervals[2 * n_local + 1];
+    const int keymask = ldu(D.ts_fw_keymask, ts), maxlevel = ldu(D.ts_fw_maxlevel, ts);
+    const double lo = ldu(D.intervals, 2 * n_local), hi = ldu(D.intervals, 2 * n_local + 1);
     double key;
     if (lo == hi) {
       key = lo;
@@ -534,12 +592,12 @@ struct Sim {
     if (mode == kScanOnly && j != jx) return false;
     if (mode == kScanExcept && j == jx) return false;
     const JobRec& jr = job(j);
-    if (!(j == src_job || jr.supply < L.num_executors)) return false;
+    if (!(j == src_job || jr.supply < NE)) return false;
     if (s.sel) return false;
     if (s.rem - (s.mov + s.com) <= 0) return false;
     const int base = jr.base;
-    for (int k = D.ts_parent_base[s.ts]; k < D.ts_parent_base[s.ts + 1]; ++k) {
-      const StageRec ps = stage(base + D.ts_parents[k]);
+    for (int k = ldg(D.ts_parent_base, s.ts); k < ldg(D.ts_parent_base, s.ts + 1); ++k) {
+      const StageRec ps = stage(base + ldg(D.ts_parents, k));
       if (ps.rem - (ps.mov + ps.com) > 0) return false;
     }
     return true;
@@ -638,7 +696,7 @@ struct Sim {
     if (!is_stage_pool(src) && !sat) return;
     const int dst = sat ? kPoolCommon : job_pool(j);
     for (int k = 0; k < n; ++k) {
-      const int e = ids[k];
+      const int e = ld(ids + k);
       move_to_pool(e, dst, false);
       if (dst == kPoolCommon) detach(j, e);
     }
@@ -657,7 +715,7 @@ struct Sim {
   }
 
   __device__ __forceinline__ void goto_stage(int e, int g) {  // _move_executor_to_stage :799-819 (+ backup loop)
-    for (int guard = 0; guard < 4 * L.stage_cap + 8; ++guard) {
+    for (int guard = 0; guard < 4 * SC + 8; ++guard) {
       if (st_rem(g) == 0) {  // _try_backup_schedule :784-797
         const int b = find_backup(e);
         if (b >= 0) {
@@ -700,11 +758,11 @@ struct Sim {
     const int n_plan = h.source >= 0 ? commit_plan(h.source, plan) : 0;
     int k = 0;
     for (int c = 0; c < n_plan; ++c) {
-      const int dst = plan[2 * c];
-      int n = plan[2 * c + 1];
+      const int dst = ld(plan + 2 * c);
+      int n = ld(plan + 2 * c + 1);
       check(dst >= 0 && n > 0);
       while (n > 0 && k < n_idle && !frozen()) {
-        const int e = idle[k++];
+        const int e = ld(idle + k++);
         fulfill(e, dst);
         n--;
       }
@@ -769,8 +827,9 @@ struct Sim {
     job_nact(j) -= 1;
     const int ts = st_ts(g), base = job_base(j);
     bool changed = false;
-    for (int k = D.ts_child_base[ts]; k < D.ts_child_base[ts + 1]; ++k) {
-      const int c = base + D.ts_children[k];
+    const int kb = ldu(D.ts_child_base, ts), ke = ldu(D.ts_child_base, ts + 1);
+    for (int k = kb; k < ke; ++k) {
+      const int c = base + ldu(D.ts_children, k);
       st_unmet(c) -= 1;
       if (st_unmet(c) == 0 && !st_completed(c)) changed = true;
     }
@@ -812,12 +871,18 @@ struct Sim {
   __device__ __forceinline__ bool pop_event(double* t, int* kind, int* e, int* g, int* seq) {
     double bt = 0.0;
     int bseq = 0x7FFFFFFF, be = -1;
-    for (int k0 = 0; k0 < L.num_executors; k0 += W::kWidth) {
+    for (int k0 = 0; k0 < NE; k0 += W::kWidth) {
       const int k = k0 + W::lane();
-      const bool ok = k < L.num_executors && ev_seq(k) >= 0;
-      double tt = ok ? ev_t(k) : __builtin_inf();
-      int ss = ok ? ev_seq(k) : 0x7FFFFFFF;
-      int kk = ok ? k : -1;
+      double tt = __builtin_inf();
+      int ss = 0x7FFFFFFF, kk = -1;
+      if (k < NE) {
+        const ExecRec r = exr(k);
+        if (r.ev_seq >= 0) {
+          tt = r.ev_t;
+          ss = r.ev_seq;
+          kk = k;
+        }
+      }
       W::min_event(tt, ss, kk);
       if (kk >= 0 && (be < 0 || tt < bt || (tt == bt && ss < bseq))) {
         bt = tt;
@@ -898,13 +963,14 @@ struct Sim {
     for (int j0 = 0; j0 < h.arrivals; j0 += W::kWidth) {
       const int j = j0 + W::lane();
       if (j < h.arrivals) {
-        const int st = job_state(j);
-        const bool in_union =
-            st == kJobActive || (st == kJobDone && job_done_dec(j) == dec && job_arr_dec(j) < dec);
+        const JobRec jr = job(j);
+        const JobTimes jt = jtimes(j);
+        const int st = jr.state;
+        const bool in_union = st == kJobActive || (st == kJobDone && jr.done_dec == dec && jr.arr_dec < dec);
         if (in_union) {
-          const double ta = job_tarr(j);
+          const double ta = jt.tarr;
           const double a = ta > t0 ? ta : t0;
-          const double tc = st == kJobDone ? job_tdone(j) : h.wall;
+          const double tc = st == kJobDone ? jt.tdone : h.wall;
           const double b = tc < h.wall ? tc : h.wall;
           if (C.beta == 0.0)
             part += b - a;
@@ -925,9 +991,9 @@ struct Sim {
     const int16_t* act = H<int16_t>(O.active_stages);
     int16_t* sched = H<int16_t>(O.sched_list);
     int16_t* row_of = S<int16_t>(O.sc_row_of);
-    float* nodes = reinterpret_cast<float*>(obs + L.ob_nodes) + (int64_t)eid * L.stage_cap * 3;
-    uint8_t* front = obs + L.ob_frontier + (int64_t)eid * L.stage_cap;
-    int32_t* srank = reinterpret_cast<int32_t*>(obs + L.ob_sched_rank) + (int64_t)eid * L.stage_cap;
+    float* nodes = reinterpret_cast<float*>(obs + L.ob_nodes) + (int64_t)eid * SC * 3;
+    uint8_t* front = obs + L.ob_frontier + (int64_t)eid * SC;
+    int32_t* srank = reinterpret_cast<int32_t*>(obs + L.ob_sched_rank) + (int64_t)eid * SC;
     int nsched = 0;
     for (int i0 = 0; i0 < n; i0 += W::kWidth) {
       const int i = i0 + W::lane();
@@ -937,10 +1003,11 @@ struct Sim {
       const uint64_t m = W::ballot(s);
       const int r = nsched + W::rank(m);
       if (ok) {
-        nodes[3 * i + 0] = (float)st_rem(g);
-        nodes[3 * i + 1] = (float)st_recent(g);
+        const StageRec sr = stage(g);
+        nodes[3 * i + 0] = (float)sr.rem;
+        nodes[3 * i + 1] = (float)recent()[g];
         nodes[3 * i + 2] = s ? 1.0f : 0.0f;
-        front[i] = st_unmet(g) == 0 ? 1 : 0;
+        front[i] = sr.unmet == 0 ? 1 : 0;
         srank[i] = s ? r : -1;
         row_of[g] = (int16_t)i;
         if (s) sched[r] = (int16_t)g;
@@ -951,19 +1018,20 @@ struct Sim {
     // jobs: dag_ptr, exec_supplies, source_job_idx
     const int nj = h.n_active_jobs;
     const int16_t* aj = H<int16_t>(O.active_jobs);
-    int32_t* ptr = reinterpret_cast<int32_t*>(obs + L.ob_dag_ptr) + (int64_t)eid * (L.job_cap + 1);
-    int32_t* sup = reinterpret_cast<int32_t*>(obs + L.ob_supplies) + (int64_t)eid * L.job_cap;
+    int32_t* ptr = reinterpret_cast<int32_t*>(obs + L.ob_dag_ptr) + (int64_t)eid * (JC + 1);
+    int32_t* sup = reinterpret_cast<int32_t*>(obs + L.ob_supplies) + (int64_t)eid * JC;
     int src_idx = nj, run = 0;
     for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
       const int k = k0 + W::lane();
       const bool ok = k < nj;
       const int j = ok ? aj[k] : -1;
-      const int cnt = ok ? job_nact(j) : 0;
+      const JobRec jr = ok ? job(j) : JobRec{};
+      const int cnt = ok ? jr.nact : 0;
       int total = 0;
       const int ex = W::excl_scan(cnt, &total);
       if (ok) {
         ptr[k] = run + ex;
-        sup[k] = job_supply(j);
+        sup[k] = jr.supply;
       }
       const uint64_t ms = W::ballot(ok && j == src_job);
       if (ms) src_idx = k0 + W::ffs(ms);
@@ -980,20 +1048,23 @@ struct Sim {
       const int g = ok ? act[i] : -1;
       int cnt = 0, cb = 0, ce = 0, base = 0;
       if (ok) {
-        const int ts = st_ts(g);
-        base = job_base(st_job(g));
-        cb = D.ts_child_base[ts];
-        ce = D.ts_child_base[ts + 1];
-        for (int k = cb; k < ce; ++k)
-          if (!st_completed(base + D.ts_children[k])) cnt++;
+        const StageRec sr = stage(g);
+        base = job(sr.job).base;
+        cb = ldg(D.ts_child_base, sr.ts);
+        ce = ldg(D.ts_child_base, sr.ts + 1);
+        for (int k = cb; k < ce; ++k) {
+          const StageRec c = stage(base + ldg(D.ts_children, k));
+          if (!(c.rem == 0 && c.exe == 0)) cnt++;
+        }
       }
       int total = 0;
       const int ex = W::excl_scan(cnt, &total);
       if (ok) {
         int o = ne + ex;
         for (int k = cb; k < ce; ++k) {
-          const int c = base + D.ts_children[k];
-          if (!st_completed(c) && o < L.edge_cap) {
+          const int c = base + ldg(D.ts_children, k);
+          const StageRec cr = stage(c);
+          if (!(cr.rem == 0 && cr.exe == 0) && o < L.edge_cap) {
             links[2 * o + 0] = i;
             links[2 * o + 1] = row_of[c];
             o++;
@@ -1056,7 +1127,7 @@ struct Sim {
     SSIM_TIC(t_act);
     const int idx = a.stage_idx, nx = a.num_exec;
     // Discrete(n, start=-1) holds -1 .. n-2; Discrete(N, start=1) holds 1 .. N
-    if (idx < -1 || idx > h.stage_idx_n - 2 || nx < 1 || nx > L.num_executors) {
+    if (idx < -1 || idx > h.stage_idx_n - 2 || nx < 1 || nx > NE) {
       write_err_only(SSIM_ERR_SPACE);
       return;
     }
@@ -1067,7 +1138,7 @@ struct Sim {
         write_err_only(SSIM_ERR_KEY);
         return;
       }
-      const int g = H<int16_t>(O.sched_list)[idx];
+      const int g = ld(H<int16_t>(O.sched_list) + idx);
       if (nx > committable()) {
         write_err_only(SSIM_ERR_TOO_MANY);
         return;
@@ -1077,7 +1148,7 @@ struct Sim {
       check(n > 0);
       add_commitment(n, stage_pool(g));
       st_sel(g) = 1;
-      if (h.n_selected <= L.num_executors) {
+      if (h.n_selected <= NE) {
         if (W::lane() == 0) H<int16_t>(O.sel_list)[h.n_selected] = (int16_t)g;
         h.n_selected++;
       } else {
@@ -1130,7 +1201,7 @@ struct Sim {
   __device__ __forceinline__ void reset(const uint8_t* rec_base) {
     const ssim_reset_record* rec = reinterpret_cast<const ssim_reset_record*>(rec_base);
     const double* tarr = reinterpret_cast<const double*>(rec_base + kResetHeadBytes);
-    const int32_t* tpl = reinterpret_cast<const int32_t*>(rec_base + kResetHeadBytes + 8 * (int64_t)L.job_cap);
+    const int32_t* tpl = reinterpret_cast<const int32_t*>(rec_base + kResetHeadBytes + 8 * (int64_t)JC);
     const int nj = rec->num_jobs;
     if (nj <= 0) return;
     const int prev_episode = H<EnvHeader>(O.hdr)->episode;
@@ -1147,7 +1218,7 @@ struct Sim {
     h.seq = nj;
     h.source = kPoolCommon;
     h.commit_seq = 0;
-    if (nj > L.job_cap) {
+    if (nj > JC) {
       fail(SSIM_ERR_RESET);
       h.num_jobs = 0;
       observe(0.0);
@@ -1162,7 +1233,7 @@ struct Sim {
       const bool ok = j < nj;
       const int t = ok ? tpl[j] : 0;
       const bool tb = ok && (t < 0 || t >= D.num_templates);
-      const int ns = (ok && !tb) ? D.tpl_stage_base[t + 1] - D.tpl_stage_base[t] : 0;
+      const int ns = (ok && !tb) ? ldg(D.tpl_stage_base, t + 1) - ldg(D.tpl_stage_base, t) : 0;
       int total = 0;
       const int ex = W::excl_scan(ns, &total);
       if (ok) {
@@ -1182,7 +1253,7 @@ struct Sim {
       if (W::ballot(tb)) bad = true;
       run += total;
     }
-    if (bad || run > L.stage_cap) {
+    if (bad || run > SC) {
       fail(SSIM_ERR_RESET);
       h.num_jobs = 0;
       observe(0.0);
@@ -1192,27 +1263,27 @@ struct Sim {
     W::sync();
     // stages
     for (int j = 0; j < nj; ++j) {
-      const int t = job_tpl(j), base = job_base(j), ns = job_nst(j), tsb = D.tpl_stage_base[t];
+      const int t = job_tpl(j), base = job_base(j), ns = job_nst(j), tsb = ldg(D.tpl_stage_base, t);
       for (int k0 = 0; k0 < ns; k0 += W::kWidth) {
         const int k = k0 + W::lane();
         if (k < ns) {
           const int g = base + k, ts = tsb + k;
           st_job(g) = (int16_t)j;
           st_ts(g) = (int16_t)ts;
-          st_rem(g) = (int16_t)D.ts_num_tasks[ts];
+          st_rem(g) = (int16_t)ldg(D.ts_num_tasks, ts);
           st_exe(g) = 0;
           st_mov(g) = 0;
           st_com(g) = 0;
-          st_unmet(g) = (int16_t)(D.ts_parent_base[ts + 1] - D.ts_parent_base[ts]);
+          st_unmet(g) = (int16_t)(ldg(D.ts_parent_base, ts + 1) - ldg(D.ts_parent_base, ts));
           st_sel(g) = 0;
-          st_recent(g) = D.ts_rough[ts];
+          st_recent(g) = ldg(D.ts_rough, ts);
         }
       }
     }
     // executors, commitments, COMMON pool = set(range(N))
-    for (int k0 = 0; k0 < L.num_executors; k0 += W::kWidth) {
+    for (int k0 = 0; k0 < NE; k0 += W::kWidth) {
       const int e = k0 + W::lane();
-      if (e < L.num_executors) {
+      if (e < NE) {
         ex_loc(e) = kPoolCommon;
         ex_job(e) = -1;
         ex_task(e) = -1;
@@ -1223,18 +1294,15 @@ struct Sim {
         ev_stage(e) = -1;
       }
     }
-    for (int k0 = 0; k0 < L.commit_cap; k0 += W::kWidth) {
+    for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
       const int k = k0 + W::lane();
-      if (k < L.commit_cap) cm(k) = CommitRec{};
+      if (k < commit_cap_for(NE)) cm(k) = CommitRec{};
     }
     W::sync();
     {
       uint8_t* t = S<uint8_t>(O.sc_tab_p);
-      if (W::lane() == 0) {
-        ps_init(pmeta(kPoolCommon), t);
-        for (int e = 0; e < L.num_executors; ++e)
-          ps_add(pmeta(kPoolCommon), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));
-      }
+      ps_init(pmeta(kPoolCommon), t);
+      for (int e = 0; e < NE; ++e) ps_add<W>(pmeta(kPoolCommon), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));
       unstage_table(kPoolCommon, t);
     }
     cfrom(kPoolCommon) = 0;

@@ -114,21 +114,82 @@ struct TraceRec {  // one popped event
 static_assert(sizeof(TraceRec) == kTraceBytes, "trace record size");
 
 // Section offsets. hot/cold offsets are relative to the start of the hot/cold block; sc_* to the scratch.
+// Sections whose size depends only on (N executors, J jobs) come first, then the stage-count (S) ones, so
+// a kernel specialised on (N, J) sees compile-time offsets for everything but the few S-dependent sections.
 struct StateOffsets {
-  int64_t hot_bytes, cold_bytes, lds_bytes;  // lds_bytes = scratch (+ hot when LDS-resident)
+  int64_t hot_bytes, cold_bytes, scratch_bytes, env_bytes;
+  int64_t lds_bytes;        // scratch (+ hot when LDS-resident); decided by compute_layout
   int32_t lds_resident, pad;
-  int64_t hdr, jobs, jtimes, active_jobs, stages, active_stages, sched_list, execs, sel_list, commits, pools;
+  int64_t hdr, jobs, jtimes, active_jobs, execs, sel_list, commits, stages, pools, active_stages, sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/;
-  int64_t sc_row_of /*int16[S]*/, sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b,
-      sc_tab_p /*uint8[set_cap]*/;
+  int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
+      sc_row_of /*int16[S]*/;
 };
 
 constexpr int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
 
-inline int set_cap_for(int n) {  // smallest power of two > 4N (max CPython set table for N keys)
+constexpr int set_cap_for(int n) {  // smallest power of two > 4N (max CPython set table for N keys)
   int c = 8;
   while (c <= 4 * n) c <<= 1;
   return c;
+}
+constexpr int commit_cap_for(int n) { return 2 * n + 2; }
+
+// The per-env block layout as a function of (N, J, S). Single source of truth for the host layout and for
+// the device engine, which re-derives it with N and J as compile-time constants where it can.
+constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
+  StateOffsets O{};
+  const int64_t P = 1 + J + S, T = set_cap_for((int)N), C = commit_cap_for((int)N);
+  int64_t o = 0;
+  O.hdr = o;
+  o = align16(o + (int64_t)sizeof(EnvHeader));
+  O.jobs = o;
+  o = align16(o + (int64_t)sizeof(JobRec) * J);
+  O.jtimes = o;
+  o = align16(o + (int64_t)sizeof(JobTimes) * J);
+  O.active_jobs = o;
+  o = align16(o + 2 * J);
+  O.execs = o;
+  o = align16(o + (int64_t)sizeof(ExecRec) * N);
+  O.sel_list = o;
+  o = align16(o + 2 * (N + 1));
+  O.commits = o;
+  o = align16(o + (int64_t)sizeof(CommitRec) * C);
+  O.stages = o;  // last (N, J)-only offset
+  o = align16(o + (int64_t)sizeof(StageRec) * S);
+  O.pools = o;
+  o = align16(o + (int64_t)sizeof(PoolRec) * P);
+  O.active_stages = o;
+  o = align16(o + 2 * S);
+  O.sched_list = o;
+  o = align16(o + 2 * S);
+  O.hot_bytes = o;
+
+  int64_t c = 0;
+  O.st_recent = c;
+  c = align16(c + 8 * S);
+  O.pool_tab = c;
+  c = align16(c + T * P);
+  O.cold_bytes = c;
+  O.env_bytes = O.hot_bytes + O.cold_bytes;
+
+  int64_t s = 0;
+  O.sc_keys_a = s;
+  s = align16(s + 4 * (N + 1));
+  O.sc_keys_b = s;
+  s = align16(s + 4 * (N + 1));
+  O.sc_plan = s;
+  s = align16(s + 8 * C);
+  O.sc_tab_a = s;
+  s = align16(s + T);
+  O.sc_tab_b = s;
+  s = align16(s + T);
+  O.sc_tab_p = s;
+  s = align16(s + T);
+  O.sc_row_of = s;
+  s = align16(s + 2 * S);
+  O.scratch_bytes = s;
+  return O;
 }
 
 // Computes the public layout and the private offsets. Returns false on a bad / unsupported config.
@@ -137,10 +198,9 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
       cfg.max_stages <= 0 || cfg.max_stages > 255 || cfg.max_edges < 0 || cfg.trace_cap < 0)
     return false;
   memset(L, 0, sizeof(*L));
-  memset(O, 0, sizeof(*O));
   const int64_t B = cfg.num_envs, N = cfg.num_executors, J = cfg.job_cap;
   const int64_t S = J * cfg.max_stages, E = J * (cfg.max_edges > 0 ? cfg.max_edges : 1);
-  const int64_t P = 1 + J + S, T = set_cap_for((int)N), C = 2 * N + 2;
+  const int64_t P = 1 + J + S, T = set_cap_for((int)N), C = commit_cap_for((int)N);
   if (P >= 32767) return false;  // pool codes and stage indices are int16 in the hot block
   L->num_envs = (int32_t)B;
   L->num_executors = (int32_t)N;
@@ -152,54 +212,13 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
   L->commit_cap = (int32_t)C;
   L->trace_cap = cfg.trace_cap;
 
-  int64_t o = 0;
-  auto take = [&](int64_t bytes) {
-    int64_t r = o;
-    o = align16(o + bytes);
-    return r;
-  };
-  O->hdr = take(sizeof(EnvHeader));
-  O->jobs = take((int64_t)sizeof(JobRec) * J);
-  O->jtimes = take((int64_t)sizeof(JobTimes) * J);
-  O->active_jobs = take(2 * J);
-  O->stages = take((int64_t)sizeof(StageRec) * S);
-  O->active_stages = take(2 * S);
-  O->sched_list = take(2 * S);
-  O->execs = take((int64_t)sizeof(ExecRec) * N);
-  O->sel_list = take(2 * (N + 1));
-  O->commits = take((int64_t)sizeof(CommitRec) * C);
-  O->pools = take((int64_t)sizeof(PoolRec) * P);
-  O->hot_bytes = align16(o);
-
-  int64_t c = 0;
-  auto ctake = [&](int64_t bytes) {
-    int64_t r = c;
-    c = align16(c + bytes);
-    return r;
-  };
-  O->st_recent = ctake(8 * S);
-  O->pool_tab = ctake(T * P);
-  O->cold_bytes = align16(c);
-  L->env_bytes = O->hot_bytes + O->cold_bytes;
+  *O = state_offsets(N, J, S);
+  L->env_bytes = O->env_bytes;
   L->state_bytes = 4096 + L->env_bytes * B;  // params block (engine.h kParamsReserve) + env blocks
-
-  // scratch block per env (LDS)
-  int64_t s = 0;
-  auto stake = [&](int64_t bytes) {
-    int64_t r = s;
-    s = align16(s + bytes);
-    return r;
-  };
-  O->sc_row_of = stake(2 * S);
-  O->sc_keys_a = stake(4 * (N + 1));
-  O->sc_keys_b = stake(4 * (N + 1));
-  O->sc_plan = stake(8 * C);
-  O->sc_tab_a = stake(T);
-  O->sc_tab_b = stake(T);
-  O->sc_tab_p = stake(T);
-  L->scratch_bytes = align16(s);
-  O->lds_resident = (O->hot_bytes + L->scratch_bytes <= kLdsBudget) ? 1 : 0;
-  O->lds_bytes = L->scratch_bytes + (O->lds_resident ? O->hot_bytes : 0);
+  L->scratch_bytes = O->scratch_bytes;
+  // LDS per wave: [hot copy (if resident) | scratch]
+  O->lds_resident = (O->hot_bytes + O->scratch_bytes <= kLdsBudget) ? 1 : 0;
+  O->lds_bytes = O->scratch_bytes + (O->lds_resident ? O->hot_bytes : 0);
 
   // obs arena: each field is [B][per-env]
   int64_t b = 0;

@@ -24,6 +24,9 @@ struct PySetMeta {
 };
 static_assert(sizeof(PySetMeta) == 6, "pool metadata is 6 bytes in the hot block");
 
+// Execution: every lane of the wave runs these with identical (wave-uniform) keys and tables; each
+// table / metadata read goes through W::uni so the probe loops are scalar code, and writes are
+// same-address stores from all lanes (one LDS access). The 1-lane host build runs the same code.
 __device__ __forceinline__ void ps_init(PySetMeta* m, uint8_t* tab) {
   m->mask = 7;
   m->fill = 0;
@@ -32,16 +35,17 @@ __device__ __forceinline__ void ps_init(PySetMeta* m, uint8_t* tab) {
 }
 
 // set_insert_clean: table known to contain no dummies and not `key`.
+template <class W>
 __device__ __forceinline__ void ps_insert_clean(uint8_t* tab, uint32_t mask, uint32_t key) {
   uint32_t i = key & mask, perturb = key;
   for (;;) {
-    if (tab[i] == kSlotEmpty) {
+    if (W::uni(tab[i]) == kSlotEmpty) {
       tab[i] = (uint8_t)key;
       return;
     }
     if (i + 9u <= mask) {
       for (uint32_t j = 1; j <= 9u; ++j) {
-        if (tab[i + j] == kSlotEmpty) {
+        if (W::uni(tab[i + j]) == kSlotEmpty) {
           tab[i + j] = (uint8_t)key;
           return;
         }
@@ -53,49 +57,53 @@ __device__ __forceinline__ void ps_insert_clean(uint8_t* tab, uint32_t mask, uin
 }
 
 // Active keys in table order (= iteration order = pop order of a fresh set). Returns the count.
+template <class W>
 __device__ __forceinline__ int ps_keys(const PySetMeta* m, const uint8_t* tab, int32_t* out) {
   int n = 0;
-  const int size = (int)m->mask + 1;
+  const int size = (int)W::uni(m->mask) + 1;
   for (int i = 0; i < size; ++i) {
-    const uint8_t v = tab[i];
+    const uint8_t v = W::uni(tab[i]);
     if (v < kSlotDummy) out[n++] = v;
   }
   return n;
 }
 
 // set_table_resize(so, minused): clean re-insert of the active keys (old table order).
+template <class W>
 __device__ __forceinline__ void ps_resize(PySetMeta* m, uint8_t* tab, int minused, int32_t* tmp) {
-  const int n = ps_keys(m, tab, tmp);
+  const int n = ps_keys<W>(m, tab, tmp);
   uint32_t size = 8;
   while ((int)size <= minused) size <<= 1;
   for (uint32_t i = 0; i < size; ++i) tab[i] = kSlotEmpty;
   const uint32_t mask = size - 1;
-  for (int k = 0; k < n; ++k) ps_insert_clean(tab, mask, (uint32_t)tmp[k]);
+  for (int k = 0; k < n; ++k) ps_insert_clean<W>(tab, mask, (uint32_t)W::uni(tmp[k]));
   m->mask = (uint16_t)mask;
   m->fill = (uint16_t)n;
   m->used = (uint16_t)n;
 }
 
 // set_add_entry for an int key. `tmp` needs room for used+1 keys (resize scratch).
+template <class W>
 __device__ __forceinline__ void ps_add(PySetMeta* m, uint8_t* tab, uint32_t key, int32_t* tmp) {
-  const uint32_t mask = m->mask;
+  const uint32_t mask = W::uni(m->mask);
+  const uint32_t fill = W::uni(m->fill), used = W::uni(m->used);
   uint32_t i = key & mask, perturb = key;
   int freeslot = -1;
   for (;;) {
     const uint32_t probes = (i + 9u <= mask) ? 9u : 0u;
     for (uint32_t j = 0; j <= probes; ++j) {
       const uint32_t idx = i + j;
-      const uint8_t v = tab[idx];
+      const uint8_t v = W::uni(tab[idx]);
       if (v == kSlotEmpty) {
         if (freeslot >= 0) {
           tab[freeslot] = (uint8_t)key;
-          m->used++;
+          m->used = (uint16_t)(used + 1);
           return;
         }
         tab[idx] = (uint8_t)key;
-        m->fill++;
-        m->used++;
-        if ((uint32_t)m->fill * 5u >= mask * 3u) ps_resize(m, tab, (int)m->used * 4, tmp);
+        m->fill = (uint16_t)(fill + 1);
+        m->used = (uint16_t)(used + 1);
+        if ((fill + 1) * 5u >= mask * 3u) ps_resize<W>(m, tab, (int)(used + 1) * 4, tmp);
         return;
       }
       if (v == key) return;
@@ -107,17 +115,18 @@ __device__ __forceinline__ void ps_add(PySetMeta* m, uint8_t* tab, uint32_t key,
 }
 
 // set.remove(key) via set_lookkey's probe sequence. Returns false if absent (KeyError in CPython).
+template <class W>
 __device__ __forceinline__ bool ps_remove(PySetMeta* m, uint8_t* tab, uint32_t key) {
-  const uint32_t mask = m->mask;
+  const uint32_t mask = W::uni(m->mask);
   uint32_t i = key & mask, perturb = key;
   for (;;) {
     const uint32_t probes = (i + 9u <= mask) ? 9u : 0u;
     for (uint32_t j = 0; j <= probes; ++j) {
-      const uint8_t v = tab[i + j];
+      const uint8_t v = W::uni(tab[i + j]);
       if (v == kSlotEmpty) return false;
       if (v == key) {
         tab[i + j] = kSlotDummy;
-        m->used--;
+        m->used = (uint16_t)(W::uni(m->used) - 1);
         return true;
       }
     }
@@ -129,6 +138,7 @@ __device__ __forceinline__ bool ps_remove(PySetMeta* m, uint8_t* tab, uint32_t k
 // Iteration order of `src.copy()` (set_merge into a fresh set: one pre-resize to > used*2 when
 // used*5 >= 21, then slot copy if same mask and no dummies, else clean insert in source order).
 // `keys` holds src's keys in table order on entry (n of them) and the copy's order on exit.
+template <class W>
 __device__ __forceinline__ void ps_copy_order(const PySetMeta* src, int32_t* keys, int n, uint8_t* tab) {
   if (n == 0) return;
   uint32_t size = 8;
@@ -136,21 +146,24 @@ __device__ __forceinline__ void ps_copy_order(const PySetMeta* src, int32_t* key
     while ((int)size <= n * 2) size <<= 1;
   }
   const uint32_t mask = size - 1;
-  if (mask == src->mask && src->fill == src->used) return;  // slot-for-slot copy keeps the order
+  if (mask == W::uni(src->mask) && W::uni(src->fill) == W::uni(src->used)) return;  // slot copy keeps order
   for (uint32_t i = 0; i < size; ++i) tab[i] = kSlotEmpty;
-  for (int k = 0; k < n; ++k) ps_insert_clean(tab, mask, (uint32_t)keys[k]);
+  for (int k = 0; k < n; ++k) ps_insert_clean<W>(tab, mask, (uint32_t)W::uni(keys[k]));
   int c = 0;
-  for (uint32_t i = 0; i < size; ++i)
-    if (tab[i] != kSlotEmpty) keys[c++] = tab[i];
+  for (uint32_t i = 0; i < size; ++i) {
+    const uint8_t v = W::uni(tab[i]);
+    if (v != kSlotEmpty) keys[c++] = v;
+  }
 }
 
 // Table order of `set(keys)` built by sequential adds into a fresh set (no removals, so no dummies).
 // In-place on `keys` (n entries); `tab` and `tmp` are scratch.
+template <class W>
 __device__ __forceinline__ void ps_build_order(int32_t* keys, int n, uint8_t* tab, int32_t* tmp) {
   PySetMeta m;
   ps_init(&m, tab);
-  for (int k = 0; k < n; ++k) ps_add(&m, tab, (uint32_t)keys[k], tmp);
-  ps_keys(&m, tab, keys);
+  for (int k = 0; k < n; ++k) ps_add<W>(&m, tab, (uint32_t)W::uni(keys[k]), tmp);
+  ps_keys<W>(&m, tab, keys);
 }
 
 }  // namespace ssim

@@ -28,6 +28,23 @@ struct WaveHip {
   __device__ static __forceinline__ int rank(uint64_t m) {  // set bits of m below this lane
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   }
+  // Wave-uniform value -> SGPR. The serial part of the algorithm runs on values every lane holds
+  // identically; v_readfirstlane makes that provable, so its arithmetic is SALU and its branches are
+  // s_cbranch_scc instead of exec-mask (divergent) control flow.
+  __device__ static __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+  __device__ static __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ int16_t uni(int16_t v) { return (int16_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ uint16_t uni(uint16_t v) { return (uint16_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ uint8_t uni(uint8_t v) { return (uint8_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ uint64_t uni(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+  }
+  __device__ static __forceinline__ int64_t uni(int64_t v) { return (int64_t)uni((uint64_t)v); }
+  __device__ static __forceinline__ double uni(double v) {
+    return __builtin_bit_cast(double, uni(__builtin_bit_cast(uint64_t, v)));
+  }
   // v_readlane (VALU -> SGPR) instead of an LDS-path ds_bpermute; `l` is wave-uniform
   __device__ static __forceinline__ int bcast_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
   __device__ static __forceinline__ double bcast_d(double v, int l) {
@@ -114,12 +131,15 @@ __global__ __launch_bounds__(64) void k_reset(const Params* __restrict__ P, uint
   s.reset(reset + (int64_t)eid * P->L.reset_stride);
 }
 
+// kRes: hot block LDS-resident. A compile-time flag (not a runtime select between an LDS and an HBM pointer)
+// so every hot-block access compiles to ds_read/ds_write rather than FLAT instructions.
+template <bool kRes, int kN, int kJ>
 __global__ __launch_bounds__(64) void k_step(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                              const int32_t* __restrict__ stage_idx,
                                              const int32_t* __restrict__ num_exec) {
   const int eid = blockIdx.x;
   if (env_idle(P, state, eid)) return;
-  Sim<WaveHip> s(P, state, g_smem, obs, eid, P->O.lds_resident != 0);
+  Sim<WaveHip, kN, kJ> s(P, state, g_smem, obs, eid, kRes);
   StepIn a;
   a.stage_idx = stage_idx[eid];
   a.num_exec = num_exec[eid];
@@ -140,13 +160,14 @@ __global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, con
   }
 }
 
+template <bool kRes, int kN, int kJ>
 __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                 int kind, uint64_t seed, int num_steps, int32_t* action_log,
                                                 uint64_t* prof_out) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
   if (env_idle(P, state, eid) && action_log == nullptr) return;
-  Sim<WaveHip> s(P, state, g_smem, obs, eid, P->O.lds_resident != 0);
+  Sim<WaveHip, kN, kJ> s(P, state, g_smem, obs, eid, kRes);
   PolicyView<WaveHip> v{P->L, obs, eid};
   s.load_hot();
   const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.hot + P->O.hdr);
@@ -187,6 +208,21 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
     if (tc) tc[o] = jt[j].tdone;
     if (st) st[o] = jr[j].state;
   }
+}
+
+// Kernel variant for a layout: LDS-resident instantiations, specialised on (executors, jobs) for the
+// benchmark shape (BASELINE configs[1]: 10 executors, 50 jobs), else the generic ones.
+using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
+using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int32_t*, uint64_t*);
+static StepFn pick_step(const Params& p) {
+  if (!p.O.lds_resident) return k_step<false, 0, 0>;
+  if (p.L.num_executors == 10 && p.L.job_cap == 50) return k_step<true, 10, 50>;
+  return k_step<true, 0, 0>;
+}
+static RolloutFn pick_rollout(const Params& p) {
+  if (!p.O.lds_resident) return k_rollout<false, 0, 0>;
+  if (p.L.num_executors == 10 && p.L.job_cap == 50) return k_rollout<true, 10, 50>;
+  return k_rollout<true, 0, 0>;
 }
 
 // ------------------------------------------------------------------------------------------ C ABI
@@ -274,7 +310,7 @@ extern "C" int ssim_reset(ssim_handle* h, void* stream) {
 extern "C" int ssim_step(ssim_handle* h, const int32_t* stage_idx, const int32_t* num_exec, void* stream) {
   if (h == nullptr || stage_idx == nullptr || num_exec == nullptr) return set_err(SSIM_E_ARG, "ssim_step: null");
   const ssim_layout& L = h->params.L;
-  hipLaunchKernelGGL(k_step, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(pick_step(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, stage_idx, num_exec);
   return hip_check(hipGetLastError(), "k_step launch");
 }
@@ -296,7 +332,7 @@ extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t
   if (kind != SSIM_POLICY_FAIR && kind != SSIM_POLICY_FIFO && kind != SSIM_POLICY_RANDOM)
     return set_err(SSIM_E_ARG, "ssim_rollout: unknown policy %d", kind);
   const ssim_layout& L = h->params.L;
-  hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, action_log, (uint64_t*)nullptr);
   return hip_check(hipGetLastError(), "k_rollout launch");
 }
@@ -306,7 +342,7 @@ extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t
 extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
                                      uint64_t* prof_out, void* stream) {
   const ssim_layout& L = h->params.L;
-  hipLaunchKernelGGL(k_rollout, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, (int32_t*)nullptr, prof_out);
   return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
 }

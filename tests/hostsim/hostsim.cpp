@@ -27,6 +27,10 @@ struct WaveSerial {
   static int ffs(uint64_t m) { return m ? __builtin_ctzll(m) : -1; }
   static int popc(uint64_t m) { return __builtin_popcountll(m); }
   static int rank(uint64_t) { return 0; }
+  template <class T>
+  static T uni(T v) {
+    return v;
+  }
   static int bcast_i(int v, int) { return v; }
   static void sync() {}
   static uint64_t clock() { return 0; }
@@ -182,14 +186,14 @@ int hs_pyset_trace(const int32_t* ops, int n_ops, int width, int32_t* orders) {
   for (int k = 0; k < n_ops; ++k) {
     const int code = ops[2 * k], key = ops[2 * k + 1];
     if (code == 0) {
-      ps_add(&m, tab, (uint32_t)key, tmp);
+      ps_add<WaveSerial>(&m, tab, (uint32_t)key, tmp);
     } else if (code == 1) {
-      if (!ps_remove(&m, tab, (uint32_t)key)) return -1;
+      if (!ps_remove<WaveSerial>(&m, tab, (uint32_t)key)) return -1;
     } else if (code == 2) {  // s = s.copy()
-      int n = ps_keys(&m, tab, keys);
+      int n = ps_keys<WaveSerial>(&m, tab, keys);
       memcpy(tab2, tab, (size_t)m.mask + 1);
       PySetMeta src = m;
-      ps_copy_order(&src, keys, n, tab2);
+      ps_copy_order<WaveSerial>(&src, keys, n, tab2);
       // materialise the copy as the current set (ps_copy_order left the copy's table in tab2 unless
       // it was a slot-for-slot copy of the source table)
       uint32_t size = 8;
@@ -204,12 +208,12 @@ int hs_pyset_trace(const int32_t* ops, int n_ops, int width, int32_t* orders) {
       m.fill = m.used = (uint16_t)n;
       finger = 0;
     } else if (code == 3) {  // s = set(x for x in s if mask bit)
-      int n = ps_keys(&m, tab, keys);
+      int n = ps_keys<WaveSerial>(&m, tab, keys);
       int c = 0;
       for (int i = 0; i < n; ++i)
         if ((key >> (keys[i] % 31)) & 1) keys[c++] = keys[i];
       ps_init(&m, tab);
-      for (int i = 0; i < c; ++i) ps_add(&m, tab, (uint32_t)keys[i], tmp);
+      for (int i = 0; i < c; ++i) ps_add<WaveSerial>(&m, tab, (uint32_t)keys[i], tmp);
       finger = 0;
     } else if (code == 4) {  // pop
       if (m.used == 0) return -2;
@@ -219,7 +223,7 @@ int hs_pyset_trace(const int32_t* ops, int n_ops, int width, int32_t* orders) {
       m.used--;
       finger = i + 1;
     }
-    int n = ps_keys(&m, tab, keys);
+    int n = ps_keys<WaveSerial>(&m, tab, keys);
     if (n > width) return -3;
     for (int i = 0; i < width; ++i) orders[(int64_t)k * width + i] = i < n ? keys[i] : -1;
   }
