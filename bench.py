@@ -68,6 +68,26 @@ def cpu_baseline(seconds: float, procs: int) -> dict:
                       "numpy Generator), mirroring trainers/rollout_worker.py"}
 
 
+def pmc_traffic(kernel: str, mode: str, envs: int, decisions_per_launch: float):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*/pmc_summary*.json,
+    made by scripts/pmc_profile.sh + scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
+    separate passes), scaled from bytes/decision to this launch. None if no matching summary."""
+    import glob
+
+    best = None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_summary*.json"))):
+        try:
+            k = json.load(open(path))["kernels"][kernel]
+        except (KeyError, ValueError, OSError):
+            continue
+        cfg = k.get("config") or {}
+        if cfg.get("mode") == mode and cfg.get("envs_per_gpu") == envs and "hbm_bytes_per_decision" in k:
+            best = (path, k["hbm_bytes_per_decision"])
+    if best is None:
+        return None, None
+    return best[1] * decisions_per_launch, os.path.relpath(best[0], REPO)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,6 +95,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
     ap.add_argument("--mode", choices=["rollout", "step"], default="rollout")
+    ap.add_argument("--chunk", type=int, default=50,
+                    help="rollout mode: steps per fused launch (warmup and timed launches all this long, so the "
+                         "rocprof per-launch average equals the timed launches' duration)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -103,13 +126,18 @@ def main():
     kind = _abi.SSIM_POLICY_RANDOM
     stream = torch.cuda.current_stream(dev)
 
+    def chunks(n):
+        c = max(1, args.chunk)
+        return [c] * (n // c) + ([n % c] if n % c else [])
+
     def run(n, events=None):
         if args.mode == "rollout":
-            if events is not None:
-                events[0].record(stream)
-            eng.rollout(kind, 1234, n)
-            if events is not None:
-                events[1].record(stream)
+            for k, c in enumerate(chunks(n)):
+                if events is not None:
+                    events[2 * k].record(stream)
+                eng.rollout(kind, 1234, c)
+                if events is not None:
+                    events[2 * k + 1].record(stream)
         else:
             for k in range(n):
                 si, ne = eng.policy(kind, 1234, run.counter)
@@ -125,7 +153,8 @@ def main():
     torch.cuda.synchronize(dev)
     counts0 = eng.views["counts"].cpu().numpy().copy()
     acc0 = eng.views["acc"].cpu().numpy().copy()
-    n_ev = 2 if args.mode == "rollout" else 2 * K
+    launches = len(chunks(K)) if args.mode == "rollout" else K
+    n_ev = 2 * launches
     events = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
     if world > 1:
         dist.barrier()
@@ -144,12 +173,7 @@ def main():
     d_acc = (acc1 - acc0).sum(axis=0).astype(np.float64)  # S_act, E_act, J_act, events
     # B_dec = 36 S_act + 20 E_act + 16 J_act + 96 K + 40 bytes per decision
     alg_bytes = 36 * d_acc[0] + 20 * d_acc[1] + 16 * d_acc[2] + 96 * d_acc[3] + 40 * decisions
-    if args.mode == "rollout":
-        kern_ms = events[0].elapsed_time(events[1])
-        launches = 1
-    else:
-        kern_ms = sum(events[2 * k].elapsed_time(events[2 * k + 1]) for k in range(K))
-        launches = K
+    kern_ms = sum(events[2 * k].elapsed_time(events[2 * k + 1]) for k in range(launches))
     elapsed = t1 - t0
     stats = torch.tensor([elapsed, float(decisions), alg_bytes, kern_ms, float(errs), float(terminated)],
                          dtype=torch.float64, device=dev)
@@ -168,6 +192,8 @@ def main():
     kern_ms = kern_ms_sum / world
     value = decisions / elapsed
     achieved = (alg_bytes / world / launches) / (kern_ms / launches / 1e3) / 1e9  # GB/s per GPU, dominant kernel
+    kernel = "k_rollout" if args.mode == "rollout" else "k_step"
+    traffic, traffic_src = pmc_traffic(kernel, args.mode, B, decisions / world / launches)
     if rank == 0:
         line = {
             "metric": "scheduling decisions/sec (env steps/s)",
@@ -184,13 +210,14 @@ def main():
             "data": "synthetic TPC-H-format dataset (seeded generator), random valid actions (device RNG)",
             "config": {"workload": f"{B} envs/GPU x TPC-H 50 jobs / 10 executors (BASELINE configs[1])",
                        "envs_per_gpu": B, "jobs": 50, "executors": 10, "mode": args.mode,
+                       "steps_per_launch": args.chunk if args.mode == "rollout" else 1,
                        "parallelism": f"env-sharded x{world}"},
             "decisions": int(decisions),
             "terminated_envs": int(terminated),
             "frozen_envs": int(errs),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_rollout" if args.mode == "rollout" else "k_step",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": kernel,
                          "kernel_ms_per_launch": kern_ms / launches,
                          "alg_bytes_per_launch": alg_bytes / world / launches},
             "cpu_baseline": None,

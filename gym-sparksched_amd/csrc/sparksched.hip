@@ -14,105 +14,11 @@
 
 #include "sparksched.h"
 #include "engine.h"
+#include "decima.h"
 #include "policy.h"
+#include "wave_hip.h"
 
 using namespace ssim;
-
-// ------------------------------------------------------------------------------------------ wave ops
-struct WaveHip {
-  static constexpr int kWidth = 64;
-  __device__ static __forceinline__ int lane() { return (int)__lane_id(); }
-  __device__ static __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
-  __device__ static __forceinline__ int ffs(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
-  __device__ static __forceinline__ int popc(uint64_t m) { return __popcll((unsigned long long)m); }
-  __device__ static __forceinline__ int rank(uint64_t m) {  // set bits of m below this lane
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  }
-  // Wave-uniform value -> SGPR. The serial part of the algorithm runs on values every lane holds
-  // identically; v_readfirstlane makes that provable, so its arithmetic is SALU and its branches are
-  // s_cbranch_scc instead of exec-mask (divergent) control flow.
-  __device__ static __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-  __device__ static __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-  __device__ static __forceinline__ int16_t uni(int16_t v) { return (int16_t)__builtin_amdgcn_readfirstlane((int)v); }
-  __device__ static __forceinline__ uint16_t uni(uint16_t v) { return (uint16_t)__builtin_amdgcn_readfirstlane((int)v); }
-  __device__ static __forceinline__ uint8_t uni(uint8_t v) { return (uint8_t)__builtin_amdgcn_readfirstlane((int)v); }
-  __device__ static __forceinline__ uint64_t uni(uint64_t v) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-  }
-  __device__ static __forceinline__ int64_t uni(int64_t v) { return (int64_t)uni((uint64_t)v); }
-  __device__ static __forceinline__ double uni(double v) {
-    return __builtin_bit_cast(double, uni(__builtin_bit_cast(uint64_t, v)));
-  }
-  // v_readlane (VALU -> SGPR) instead of an LDS-path ds_bpermute; `l` is wave-uniform
-  __device__ static __forceinline__ int bcast_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-  __device__ static __forceinline__ double bcast_d(double v, int l) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-  }
-  __device__ static __forceinline__ void sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  __device__ static __forceinline__ uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
-  __device__ static __forceinline__ int excl_scan(int x, int* total) {
-    int v = x;
-    const int l = lane();
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(v, (unsigned)off);
-      if (l >= off) v += y;
-    }
-    *total = __shfl(v, 63);
-    return v - x;
-  }
-  __device__ static __forceinline__ double sum_d(double x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-    return x;
-  }
-  // Sparse argmins: the candidates are few (live commitments, pending executor events), so walk the
-  // ballot of valid lanes with v_readlane instead of a 6-round ds_bpermute butterfly.
-  // lexicographic min of (key, val) over lanes with key != INT_MAX; result in every lane
-  __device__ static __forceinline__ void min_pair(int& key, int& val) {
-    uint64_t m = ballot(key != 0x7FFFFFFF);
-    int bk = 0x7FFFFFFF, bv = val;
-    while (m) {
-      const int l = ffs(m);
-      m &= m - 1;
-      const int k2 = bcast_i(key, l), v2 = bcast_i(val, l);
-      if (k2 < bk || (k2 == bk && v2 < bv)) {
-        bk = k2;
-        bv = v2;
-      }
-    }
-    key = bk;
-    val = bv;
-  }
-  // min of (t, seq) with payload idx over lanes with idx >= 0; result in every lane
-  __device__ static __forceinline__ void min_event(double& t, int& seq, int& idx) {
-    uint64_t m = ballot(idx >= 0);
-    double bt = t;
-    int bs = 0x7FFFFFFF, bi = -1;
-    while (m) {
-      const int l = ffs(m);
-      m &= m - 1;
-      const double t2 = bcast_d(t, l);
-      const int s2 = bcast_i(seq, l);
-      if (bi < 0 || t2 < bt || (t2 == bt && s2 < bs)) {
-        bt = t2;
-        bs = s2;
-        bi = bcast_i(idx, l);
-      }
-    }
-    t = bt;
-    seq = bs;
-    idx = bi;
-  }
-};
 
 // ------------------------------------------------------------------------------------------ kernels
 extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
@@ -193,6 +99,13 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
 #else
   (void)prof_out;
 #endif
+}
+
+__global__ __launch_bounds__(64) void k_decima(const Params* __restrict__ P, const uint8_t* obs, float nts,
+                                               float ws, float* feats, int32_t* ccap, uint32_t* emask,
+                                               int32_t* depth) {
+  DecimaView<WaveHip> v{P->L, obs, (int)blockIdx.x};
+  v.run(nts, ws, g_smem, feats, ccap, emask, depth);
 }
 
 // per-job arrival/completion times and state (JobRec/JobTimes in the hot block) -> [num_envs][job_cap]
@@ -353,6 +266,21 @@ extern "C" int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_compl
   hipLaunchKernelGGL(k_job_times, dim3(h->params.L.num_envs), dim3(64), 0, (hipStream_t)stream, dparams(h), h->state,
                      t_arrival, t_completed, state);
   return hip_check(hipGetLastError(), "k_job_times launch");
+}
+
+extern "C" int ssim_decima_features(ssim_handle* h, float num_tasks_scale, float work_scale, float* node_feats,
+                                    int32_t* commit_cap, uint32_t* edge_mask, int32_t* depth, void* stream) {
+  if (h == nullptr || node_feats == nullptr || commit_cap == nullptr || edge_mask == nullptr || depth == nullptr)
+    return set_err(SSIM_E_ARG, "ssim_decima_features: null argument");
+  const ssim_layout& L = h->params.L;
+  if (h->params.C.max_stages > kDecimaMaxDepth)
+    return set_err(SSIM_E_ARG, "ssim_decima_features: max_stages %d > %d (edge-mask word)", h->params.C.max_stages,
+                   kDecimaMaxDepth);
+  const int64_t lds = decima_scratch_bytes(L.stage_cap);
+  if (lds > kLdsBudget) return set_err(SSIM_E_ARG, "ssim_decima_features: stage_cap %d too large", L.stage_cap);
+  hipLaunchKernelGGL(k_decima, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream, dparams(h), h->obs,
+                     num_tasks_scale, work_scale, node_feats, commit_cap, edge_mask, depth);
+  return hip_check(hipGetLastError(), "k_decima launch");
 }
 
 extern "C" const char* ssim_last_error(void) { return g_err; }

@@ -1,0 +1,114 @@
+// wave_hip.h — the gfx950 wave policy (W) for the engine templates: one 64-lane wavefront per env.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct WaveHip {
+  static constexpr int kWidth = 64;
+  __device__ static __forceinline__ int lane() { return (int)__lane_id(); }
+  __device__ static __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
+  __device__ static __forceinline__ int ffs(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
+  __device__ static __forceinline__ int popc(uint64_t m) { return __popcll((unsigned long long)m); }
+  __device__ static __forceinline__ int rank(uint64_t m) {  // set bits of m below this lane
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  }
+  // Wave-uniform value -> SGPR. The serial part of the algorithm runs on values every lane holds
+  // identically; v_readfirstlane makes that provable, so its arithmetic is SALU and its branches are
+  // s_cbranch_scc instead of exec-mask (divergent) control flow.
+  __device__ static __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+  __device__ static __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ int16_t uni(int16_t v) { return (int16_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ uint16_t uni(uint16_t v) { return (uint16_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ uint8_t uni(uint8_t v) { return (uint8_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ uint64_t uni(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+  }
+  __device__ static __forceinline__ int64_t uni(int64_t v) { return (int64_t)uni((uint64_t)v); }
+  __device__ static __forceinline__ double uni(double v) {
+    return __builtin_bit_cast(double, uni(__builtin_bit_cast(uint64_t, v)));
+  }
+  // v_readlane (VALU -> SGPR) instead of an LDS-path ds_bpermute; `l` is wave-uniform
+  __device__ static __forceinline__ int bcast_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+  __device__ static __forceinline__ double bcast_d(double v, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+  }
+  __device__ static __forceinline__ void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ static __forceinline__ uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+  __device__ static __forceinline__ int excl_scan(int x, int* total) {
+    int v = x;
+    const int l = lane();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(v, (unsigned)off);
+      if (l >= off) v += y;
+    }
+    *total = __shfl(v, 63);
+    return v - x;
+  }
+  __device__ static __forceinline__ double sum_d(double x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    return x;
+  }
+  // Sparse argmins: the candidates are few (live commitments, pending executor events), so walk the
+  // ballot of valid lanes with v_readlane instead of a 6-round ds_bpermute butterfly.
+  // lexicographic min of (key, val) over lanes with key != INT_MAX; result in every lane
+  __device__ static __forceinline__ void min_pair(int& key, int& val) {
+    uint64_t m = ballot(key != 0x7FFFFFFF);
+    int bk = 0x7FFFFFFF, bv = val;
+    while (m) {
+      const int l = ffs(m);
+      m &= m - 1;
+      const int k2 = bcast_i(key, l), v2 = bcast_i(val, l);
+      if (k2 < bk || (k2 == bk && v2 < bv)) {
+        bk = k2;
+        bv = v2;
+      }
+    }
+    key = bk;
+    val = bv;
+  }
+  // min of (t, seq) with payload idx over lanes with idx >= 0; result in every lane
+  __device__ static __forceinline__ void min_event(double& t, int& seq, int& idx) {
+    uint64_t m = ballot(idx >= 0);
+    double bt = t;
+    int bs = 0x7FFFFFFF, bi = -1;
+    while (m) {
+      const int l = ffs(m);
+      m &= m - 1;
+      const double t2 = bcast_d(t, l);
+      const int s2 = bcast_i(seq, l);
+      if (bi < 0 || t2 < bt || (t2 == bt && s2 < bs)) {
+        bt = t2;
+        bs = s2;
+        bi = bcast_i(idx, l);
+      }
+    }
+    t = bt;
+    seq = bs;
+    idx = bi;
+  }
+  // correctly rounded f32 ops (the reference's numpy float32 arithmetic; no contraction)
+  __device__ static __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+  __device__ static __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+  // LDS atomics / loads for lane-parallel relaxations
+  __device__ static __forceinline__ int lds_load(const int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+  __device__ static __forceinline__ void amax(int* p, int v) { atomicMax(p, v); }
+  __device__ static __forceinline__ void aor(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+  __device__ static __forceinline__ int max_i(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const int y = __shfl_xor(x, off);
+      x = y > x ? y : x;
+    }
+    return x;
+  }
+};

@@ -97,6 +97,29 @@ def obs_dict(v: dict, env: int) -> dict:
     }
 
 
+def decima_obs_dict(v: dict, dec: dict, env: int, num_executors: int) -> dict:
+    """Reference-format Decima observation of one env (schedulers/decima/env_wrapper.py:98-104) from host
+    obs views `v` and host copies `dec` of the ssim_decima_features outputs. Edge masks are the bit planes
+    of the per-edge mask words: edge_masks[l, e] = bit l of edge_mask[e], l < depth - 1."""
+    c = v["counts"][env]
+    n, ne, nj = int(c[_abi.OC_NUM_NODES]), int(c[_abi.OC_NUM_EDGES]), int(c[_abi.OC_NUM_JOBS])
+    links = np.array(v["edge_links"][env, :ne], dtype=np.int64).reshape(ne, 2)
+    caps = np.asarray(dec["commit_cap"][env, :nj], dtype=np.int64)
+    depth = int(dec["depth"][env])
+    if depth < 0:
+        raise ValueError("DAG depth exceeds the 32-level edge-mask word")
+    words = np.asarray(dec["edge_mask"][env, :ne]).astype(np.uint32)
+    levels = np.arange(max(depth - 1, 0), dtype=np.uint32)
+    return {
+        "dag_batch": GraphInstance(np.array(dec["node_feats"][env, :n], dtype=np.float32).reshape(n, 5),
+                                   np.zeros(ne, dtype=np.int64), links),
+        "dag_ptr": [int(x) for x in v["dag_ptr"][env, : nj + 1]],
+        "stage_mask": np.array(v["nodes"][env, :n, 2]).astype(bool),
+        "exec_mask": np.arange(num_executors)[None, :] < caps[:, None],
+        "edge_masks": ((words[None, :] >> levels[:, None]) & 1).astype(bool),
+    }
+
+
 try:  # gymnasium is optional; mirror its GraphInstance when absent
     from gymnasium.spaces import GraphInstance  # type: ignore
 except Exception:  # pragma: no cover - gymnasium not installed in this image
@@ -244,6 +267,29 @@ class DeviceEngine:
         self._native.check(self._native.lib().ssim_job_times(self.handle, ta.data_ptr(), tc.data_ptr(), st.data_ptr(),
                                                              self._stream()), "ssim_job_times")
         return ta, tc, st
+
+    def decima_features(self, num_tasks_scale: float = 200.0, work_scale: float = 1e5) -> dict:
+        """Decima featurisation of the current obs on device (ssim_decima_features); device tensors,
+        overwritten by the next call: node_feats f32 [B,S,5], commit_cap i32 [B,J], edge_mask i32 [B,E]
+        (uint32 bit planes stored as int32), depth i32 [B]."""
+        t = self.torch
+        L = self.layout
+        if getattr(self, "_dec", None) is None:
+            self._dec = {
+                "node_feats": t.zeros((L.num_envs, L.stage_cap, 5), dtype=t.float32, device=self.device),
+                "commit_cap": t.zeros((L.num_envs, L.job_cap), dtype=t.int32, device=self.device),
+                "edge_mask": t.zeros((L.num_envs, L.edge_cap), dtype=t.int32, device=self.device),
+                "depth": t.zeros((L.num_envs,), dtype=t.int32, device=self.device),
+            }
+        d = self._dec
+        self._native.check(self._native.lib().ssim_decima_features(
+            self.handle, float(num_tasks_scale), float(work_scale), d["node_feats"].data_ptr(),
+            d["commit_cap"].data_ptr(), d["edge_mask"].data_ptr(), d["depth"].data_ptr(), self._stream()),
+            "ssim_decima_features")
+        return d
+
+    def decima_features_np(self, num_tasks_scale: float = 200.0, work_scale: float = 1e5) -> dict:
+        return {k: x.cpu().numpy() for k, x in self.decima_features(num_tasks_scale, work_scale).items()}
 
     def job_times_np(self):
         return tuple(x.cpu().numpy() for x in self.job_times())

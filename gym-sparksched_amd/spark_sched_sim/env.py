@@ -96,6 +96,10 @@ class SparkSchedSimEnv:
 
     # -- reference properties (spark_sched_sim.py:227-245) ------------------------------------------
     @property
+    def unwrapped(self) -> "SparkSchedSimEnv":
+        return self
+
+    @property
     def info(self) -> dict:
         return {"wall_time": self.wall_time}
 

@@ -64,6 +64,12 @@ class SparkSchedSimVecEnv:
         """`num_steps` device-policy decisions per env fused into one launch."""
         self.engine.rollout(kind, seed, num_steps, action_log)
 
+    def decima_features(self, num_tasks_scale: float = 200.0, work_scale: float = 1e5) -> dict:
+        """Decima featurisation of every env's current obs, on device (schedulers/decima/env_wrapper.py:69-161):
+        node_feats f32 [B,S,5], commit_cap i32 [B,J] (exec_mask = arange(N) < cap), edge_mask [B,E] (bit l =
+        DAG-layer mask l), depth [B]. Padded rows beyond the per-env counts are unspecified."""
+        return self.engine.decima_features(num_tasks_scale, work_scale)
+
     def _info(self):
         c = self.engine.views["counts"]
         return {"wall_time": self.engine.views["wall_time"], "err": c[:, _abi.OC_ERR],

@@ -161,6 +161,17 @@ int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
  * and job state int32 [num_envs][job_cap] (0 not arrived, 1 active, 2 completed), any may be NULL. */
 int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32_t* state, void* stream);
 
+/* Decima observation features from the current obs (replaces DecimaObsWrapper.observation,
+ * schedulers/decima/env_wrapper.py:69-143, and make_dag_layer_edge_masks, schedulers/decima/utils.py:238-267).
+ * Device outputs, caller-allocated, env-major:
+ *   node_feats float [num_envs][stage_cap][5]   rows < num_nodes (the reference's 5 node features)
+ *   commit_cap int32 [num_envs][job_cap]         exec_mask[j, :commit_cap[j]] = True, rows < num_jobs
+ *   edge_mask  uint32 [num_envs][edge_cap]       bit l = edge in message-passing mask l, l < depth - 1
+ *   depth      int32 [num_envs]                  topological generations (masks are (max(depth-1,0), E))
+ * Reference defaults: num_tasks_scale 200, work_scale 1e5. Requires max_stages <= 32 (SSIM_E_ARG). */
+int ssim_decima_features(ssim_handle* h, float num_tasks_scale, float work_scale, float* node_feats,
+                         int32_t* commit_cap, uint32_t* edge_mask, int32_t* depth, void* stream);
+
 const char* ssim_last_error(void);
 
 #ifdef __cplusplus

@@ -24,7 +24,7 @@ for s in "$@"; do
     bench_step) step bench_step 300 python bench.py --no-cpu-baseline --mode step ;;
     prof)    step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     phase)   step phase 600 python scripts/phase_profile.py ;;
-    prof_step) step prof_step 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_step" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step ;;
+    prof_step) step prof_step 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_step" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

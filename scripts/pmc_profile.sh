@@ -3,20 +3,19 @@
 # sys/runtime traces). Writes under gpurun_out/pmc/<pass>/. Stops at the first fault-like exit.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/pmc
+MODE=${PMC_MODE:-rollout}
+OUT=gpurun_out/pmc_$MODE
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-MODE=${PMC_MODE:-rollout}
 run() {
   local name=$1; shift
   echo "=== pmc $name ($(date +%T))"
   timeout -k 10 300 rocprofv3 --pmc "$@" -d "$PWD/$OUT/$name" -o run --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --mode "$MODE" --steps 60 --warmup 10 > "$OUT/$name.log" 2>&1
+    python3 bench.py --no-cpu-baseline --mode "$MODE" --steps 100 --warmup 50 > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   if [ $rc -ne 0 ]; then tail -n 20 "$OUT/$name.log"; exit $rc; fi
 }
-timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 run waves SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM
 run icache SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_WAVES
 run fetch FETCH_SIZE

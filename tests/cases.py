@@ -11,10 +11,11 @@ import numpy as np
 import pytest
 
 import parity
+from oracle.decima import decima_observation
 from oracle.policies import FairPolicy, RandomPolicy
 from oracle.restatement import SparkSchedOracle
 from spark_sched_sim import _abi
-from spark_sched_sim.engine import decode_trace, obs_dict
+from spark_sched_sim.engine import decima_obs_dict, decode_trace, obs_dict
 
 LOCKSTEP_CONFIGS = [
     (dict(beta=5e-3), 4, 7, "random"),
@@ -173,3 +174,42 @@ def case_reset_continuation(make, dataset, env_cfg, B=3):
             obs[i], r, t, _, info = oracles[i].step(acts[i])
             parity.compare_obs(obs[i], obs_dict(v, i), f"env{i} step{k}")
             assert float(v["wall_time"][i]) == float(info["wall_time"])
+
+
+DECIMA_CONFIGS = [
+    (dict(), 4, 101, "random", 1),
+    (dict(num_executors=50, job_arrival_cap=200, beta=5e-3), 2, 211, "random", 5),
+    (dict(num_executors=3, job_arrival_cap=20, job_arrival_rate=1e-4, moving_delay=500.0, warmup_delay=100.0),
+     6, 307, "fair", 1),
+]
+
+
+def case_decima_features(make, dataset, env_cfg, cfg_over, B, seed0, pol, every):
+    """ssim_decima_features (node features, exec/stage masks, DAG-layer edge masks) equals the Decima
+    wrapper restatement (oracle/decima.py: env_wrapper.py:69-143, utils.py:238-267) on the oracle's
+    observation, at reset and every `every`-th decision of a full lockstep episode."""
+    cfg = dict(env_cfg, **cfg_over)
+    N = cfg["num_executors"]
+    eng = make(cfg, B, dataset, 0)
+    oracles = [SparkSchedOracle(cfg, dataset) for _ in range(B)]
+    fac = (lambda i: FairPolicy(N)) if pol == "fair" else (lambda i: RandomPolicy(900 + i))
+    seen = {"checks": 0, "masked": 0}
+
+    def hook(k, obs, live):
+        if k % every != 0:
+            return
+        dec = {key: eng.to_numpy(x) if not isinstance(x, np.ndarray) else x
+               for key, x in eng.decima_features_np().items()}
+        v = eng.host_views()
+        for i in range(B):
+            if not live[i]:
+                continue
+            ref = decima_observation(obs[i], N)
+            got = decima_obs_dict(v, dec, i, N)
+            parity.compare_decima(ref, got, f"env{i} step{k}")
+            seen["checks"] += 1
+            seen["masked"] += int(ref["edge_masks"].shape[0] > 0)
+
+    parity.run_lockstep(eng, oracles, seeds=[seed0 + i for i in range(B)], policy_factory=fac, check_every=50,
+                        hook=hook)
+    assert seen["checks"] > 50 and seen["masked"] > 10, seen

@@ -21,7 +21,7 @@ from spark_sched_sim.engine import _ResetSampler, arena_views, make_config  # no
 
 SO_PATH = os.path.join(HERE, "_hostsim.so")
 SOURCES = [os.path.join(HERE, "hostsim.cpp")] + [
-    os.path.join(REPO, "gym-sparksched_amd", "csrc", f) for f in ("engine.h", "policy.h", "pyset.h", "pcg64.h",
+    os.path.join(REPO, "gym-sparksched_amd", "csrc", f) for f in ("engine.h", "policy.h", "pyset.h", "pcg64.h", "decima.h",
                                                                   "layout.h")] + [
     os.path.join(REPO, "include", "sparksched.h")]
 
@@ -57,6 +57,7 @@ def lib():
         L.hs_pcg_run.argtypes = [vp, vp, ct.c_int, vp]
         L.hs_job_times.argtypes = [vp, vp, vp, vp]
         L.hs_pyset_trace.argtypes = [vp, ct.c_int, ct.c_int, vp]
+        L.hs_decima.argtypes = [vp, ct.c_float, ct.c_float, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -121,6 +122,17 @@ class HostEngine:
 
     def host_views(self):
         return self.views
+
+    def decima_features_np(self, num_tasks_scale: float = 200.0, work_scale: float = 1e5) -> dict:
+        L = self.layout
+        d = {"node_feats": np.zeros((L.num_envs, L.stage_cap, 5), dtype=np.float32),
+             "commit_cap": np.zeros((L.num_envs, L.job_cap), dtype=np.int32),
+             "edge_mask": np.zeros((L.num_envs, L.edge_cap), dtype=np.int32),
+             "depth": np.zeros((L.num_envs,), dtype=np.int32)}
+        lib().hs_decima(self.handle, num_tasks_scale, work_scale, *[d[k].ctypes.data for k in
+                                                                     ("node_feats", "commit_cap", "edge_mask",
+                                                                      "depth")])
+        return d
 
     def job_times_np(self):
         B, J = self.num_envs, self.cfg.job_cap

@@ -15,6 +15,7 @@ struct uint4 {  // HIP vector type used by the (device-only) LDS residency copy;
   unsigned x, y, z, w;
 };
 
+#include "decima.h"
 #include "engine.h"
 #include "policy.h"
 
@@ -39,6 +40,12 @@ struct WaveSerial {
     return 0;
   }
   static double sum_d(double x) { return x; }
+  static float fdiv(float a, float b) { return a / b; }
+  static float fmul(float a, float b) { return a * b; }
+  static int lds_load(const int* p) { return *p; }
+  static void amax(int* p, int v) { *p = v > *p ? v : *p; }
+  static void aor(uint32_t* p, uint32_t v) { *p |= v; }
+  static int max_i(int x) { return x; }
   static void min_pair(int&, int&) {}
   static void min_event(double&, int&, int&) {}
 };
@@ -150,6 +157,18 @@ void hs_job_times(hs_handle* h, double* ta, double* tc, int32_t* st) {
       st[(int64_t)e * J + j] = jr[j].state;
     }
   }
+}
+
+// Decima featurisation of the current obs (decima.h), all envs; outputs as ssim_decima_features.
+int hs_decima(hs_handle* h, float nts, float ws, float* feats, int32_t* ccap, uint32_t* emask, int32_t* depth) {
+  const Params* P = h->params;
+  uint8_t* scratch = (uint8_t*)calloc(1, (size_t)decima_scratch_bytes(P->L.stage_cap));
+  for (int e = 0; e < P->L.num_envs; ++e) {
+    DecimaView<WaveSerial> v{P->L, h->obs, e};
+    v.run(nts, ws, scratch, feats, ccap, emask, depth);
+  }
+  free(scratch);
+  return 0;
 }
 
 // PCG64 / CPython-set models exposed for the known-answer tests.

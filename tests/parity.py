@@ -43,15 +43,47 @@ def compare_obs(ref: dict, got: dict, where: str) -> None:
             raise Mismatch(f"{where}: {k} differ ref={ref[k]} got={got[k]}")
 
 
+def compare_decima(ref: dict, got: dict, where: str) -> None:
+    """Decima observation (schedulers/decima/env_wrapper.py:98-104): float32 features bit-exact, masks equal."""
+    rn, gn = ref["nodes"], got["dag_batch"].nodes
+    if rn.shape != gn.shape or not np.array_equal(rn.view(np.uint32), gn.view(np.uint32)):
+        bad = np.argwhere(rn.view(np.uint32) != gn.view(np.uint32)) if rn.shape == gn.shape else None
+        raise Mismatch(f"{where}: decima node features differ at {bad[:5] if bad is not None else 'shape'}\n"
+                       f"ref={rn}\ngot={gn}")
+    if not np.array_equal(ref["edge_links"], got["dag_batch"].edge_links):
+        raise Mismatch(f"{where}: decima edge_links differ")
+    if list(ref["dag_ptr"]) != list(got["dag_ptr"]):
+        raise Mismatch(f"{where}: decima dag_ptr differ")
+    for k in ("stage_mask", "exec_mask", "edge_masks"):
+        a, b = np.asarray(ref[k]), np.asarray(got[k])
+        if a.shape != b.shape or not np.array_equal(a, b):
+            raise Mismatch(f"{where}: decima {k} differ: ref shape {a.shape} got {b.shape}\nref={a.astype(int)}\n"
+                           f"got={b.astype(int)}")
+
+
 def close_rel(a: float, b: float, rtol: float = REWARD_RTOL) -> bool:
     return a == b or abs(a - b) <= rtol * max(abs(a), abs(b), 1e-300)
 
 
-def run_lockstep(engine, oracles, seeds, policy_factory=None, max_steps=10**9, check_every=1, actions_fn=None):
+def reward_close(got: float, ref: float, beta: float, n_jobs: int) -> bool:
+    """Reward agreement. beta == 0: 1e-9 relative (sums of exact f64 differences; only the set-order
+    summation differs). beta > 0 (spark_sched_sim.py:866-872): each job adds exp(-x_a) - exp(-x_b) with
+    both terms in (0, 1], then the sum is divided by beta. The reference's own rounding error is a few
+    ulp(1) per job (libm/numpy exp are faithful to <= 1 ulp, not correctly rounded, and the difference
+    cancels), so the bar is 1e-9 relative or that forward-error bound, 8 * eps * n_jobs / beta absolute."""
+    if close_rel(got, ref):
+        return True
+    return beta > 0.0 and abs(got - ref) <= 8.0 * 2.220446049250313e-16 * max(n_jobs, 1) / beta
+
+
+def run_lockstep(engine, oracles, seeds, policy_factory=None, max_steps=10**9, check_every=1, actions_fn=None,
+                 hook=None):
     """Drive B oracles and a B-env engine in lockstep.
 
     actions for each env come from `policy_factory(i)(oracle_obs)` (CPU oracle policy), unless `actions_fn`
     is given: actions_fn(step) -> (stage_idx[B], num_exec[B]) (e.g. device-policy replay).
+    `hook(k, obs, live)` runs after the reset (k = -1) and after every step with the oracle observations
+    and the envs still running before that step.
     Returns per-env number of decisions."""
     B = len(oracles)
     pols = [policy_factory(i) if policy_factory else FairPolicy(oracles[i].N) for i in range(B)]
@@ -64,6 +96,8 @@ def run_lockstep(engine, oracles, seeds, policy_factory=None, max_steps=10**9, c
     v = engine.host_views()
     for i in range(B):
         compare_obs(obs[i], obs_dict(v, i), f"env{i} reset")
+    if hook is not None:
+        hook(-1, obs, [True] * B)
     done = [False] * B
     steps = [0] * B
     for k in range(max_steps):
@@ -79,6 +113,7 @@ def run_lockstep(engine, oracles, seeds, policy_factory=None, max_steps=10**9, c
             if actions_fn is None:
                 a, _ = pols[i].schedule(obs[i])
                 si[i], ne[i] = int(a["stage_idx"]), int(a["num_exec"])
+        live = [not d for d in done]
         engine.step(si, ne)
         v = engine.host_views()
         for i in range(B):
@@ -94,7 +129,7 @@ def run_lockstep(engine, oracles, seeds, policy_factory=None, max_steps=10**9, c
             if got_wall != float(info["wall_time"]):
                 raise Mismatch(f"env{i} step{k}: wall {got_wall!r} != {info['wall_time']!r}")
             got_r = float(v["reward"][i])
-            if not close_rel(got_r, float(rew)):
+            if not reward_close(got_r, float(rew), oracles[i].beta, len(oracles[i].jobs)):
                 raise Mismatch(f"env{i} step{k}: reward {got_r!r} != {rew!r}")
             if bool(c[_abi.OC_TERMINATED]) != bool(term):
                 raise Mismatch(f"env{i} step{k}: terminated {bool(c[_abi.OC_TERMINATED])} != {term}")
@@ -103,6 +138,8 @@ def run_lockstep(engine, oracles, seeds, policy_factory=None, max_steps=10**9, c
             if int(c[_abi.OC_DECISIONS]) != oracles[i].decisions:
                 raise Mismatch(f"env{i} step{k}: decisions {int(c[_abi.OC_DECISIONS])} != {oracles[i].decisions}")
             done[i] = bool(term)
+        if hook is not None:
+            hook(k, obs, live)
     return steps
 
 

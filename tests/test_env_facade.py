@@ -111,3 +111,27 @@ def test_stochastic_time_limit_episode(dataset, env_cfg):
             assert (done, trunc) == (rdone, rtrunc) and parity.close_rel(r, rr)
             k += 1
         assert trunc or done
+
+
+def test_decima_env_wrapper_matches_reference_wrapper(dataset, env_cfg):
+    """spark_sched_sim.decima.DecimaEnvWrapper (device featurisation; host build here) vs the Decima wrapper
+    restatement on the oracle's observations, with Decima-format actions (num_exec offset by one)."""
+    from oracle.decima import decima_observation
+    from spark_sched_sim.decima import DecimaEnvWrapper
+
+    env = DecimaEnvWrapper(SparkSchedSimEnv(env_cfg, dataset, _engine_factory=host_factory()))
+    ref = R.SparkSchedOracle(env_cfg, dataset)
+    N = env_cfg["num_executors"]
+    obs, _ = env.reset(seed=4321)
+    robs, _ = ref.reset(seed=4321)
+    parity.compare_decima(decima_observation(robs, N), obs, "reset")
+    pol = RandomPolicy(5)
+    done, steps = False, 0
+    while not done:
+        a, _ = pol.schedule(robs)
+        obs, r, done, _, _ = env.step({"stage_idx": a["stage_idx"], "num_exec": a["num_exec"] - 1})
+        robs, rr, rdone, _, _ = ref.step(a)
+        assert done == rdone and parity.close_rel(r, rr)
+        parity.compare_decima(decima_observation(robs, N), obs, f"step {steps}")
+        steps += 1
+    assert steps > 100

@@ -41,3 +41,8 @@ def test_invalid_actions(make, dataset, env_cfg):
 
 def test_reset_continuation(make, dataset, env_cfg):
     cases.case_reset_continuation(make, dataset, env_cfg)
+
+
+@pytest.mark.parametrize("cfg_over,B,seed0,pol,every", cases.DECIMA_CONFIGS)
+def test_decima_features(make, dataset, env_cfg, cfg_over, B, seed0, pol, every):
+    cases.case_decima_features(make, dataset, env_cfg, cfg_over, min(B, 2), seed0, pol, every * 3)
