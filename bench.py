@@ -68,7 +68,7 @@ def cpu_baseline(seconds: float, procs: int) -> dict:
                       "numpy Generator), mirroring trainers/rollout_worker.py"}
 
 
-def pmc_traffic(kernel: str, mode: str, envs: int, decisions_per_launch: float):
+def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisions_per_launch: float):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*/pmc_summary*.json,
     made by scripts/pmc_profile.sh + scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
     separate passes), scaled from bytes/decision to this launch. None if no matching summary."""
@@ -81,7 +81,9 @@ def pmc_traffic(kernel: str, mode: str, envs: int, decisions_per_launch: float):
         except (KeyError, ValueError, OSError):
             continue
         cfg = k.get("config") or {}
-        if cfg.get("mode") == mode and cfg.get("envs_per_gpu") == envs and "hbm_bytes_per_decision" in k:
+        spl = cfg.get("steps_per_launch", k.get("steps") if mode == "rollout" else 1)
+        if (cfg.get("mode") == mode and cfg.get("envs_per_gpu") == envs and spl == steps_per_launch
+                and "hbm_bytes_per_decision" in k):
             best = (path, k["hbm_bytes_per_decision"])
     if best is None:
         return None, None
@@ -95,9 +97,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
     ap.add_argument("--mode", choices=["rollout", "step"], default="rollout")
-    ap.add_argument("--chunk", type=int, default=50,
-                    help="rollout mode: steps per fused launch (warmup and timed launches all this long, so the "
-                         "rocprof per-launch average equals the timed launches' duration)")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="rollout mode: steps per fused launch (0 = --steps). Warmup runs in launches of the same "
+                         "length (>= --warmup steps in total), so every k_rollout launch is alike and the rocprof "
+                         "per-launch average is the timed launches' duration")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -110,11 +113,10 @@ def main():
 
     from spark_sched_sim import _abi
     from spark_sched_sim.data_samplers.synthetic_tpch import generate
+    from spark_sched_sim.distributed import gather_env_stats, rank_world, reduce_timing, shard_seeds
     from spark_sched_sim.engine import DeviceEngine
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = rank_world()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", init_method="env://")
@@ -122,13 +124,14 @@ def main():
 
     B, K, W = args.envs, args.steps, args.warmup
     eng = DeviceEngine(ENV_CFG, B, generate(0), device=dev)
-    eng.reset(seeds=[args.seed + rank * B + i for i in range(B)])
+    eng.reset(seeds=shard_seeds(rank, B, args.seed))
     kind = _abi.SSIM_POLICY_RANDOM
     stream = torch.cuda.current_stream(dev)
 
+    chunk = args.chunk if args.chunk > 0 else K
+
     def chunks(n):
-        c = max(1, args.chunk)
-        return [c] * (n // c) + ([n % c] if n % c else [])
+        return [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
 
     def run(n, events=None):
         if args.mode == "rollout":
@@ -149,6 +152,8 @@ def main():
                     events[2 * k + 1].record(stream)
     run.counter = 0
 
+    if args.mode == "rollout":
+        W = -(-W // chunk) * chunk if W > 0 else 0  # whole launches of `chunk` steps
     run(W)
     torch.cuda.synchronize(dev)
     counts0 = eng.views["counts"].cpu().numpy().copy()
@@ -177,23 +182,18 @@ def main():
     elapsed = t1 - t0
     stats = torch.tensor([elapsed, float(decisions), alg_bytes, kern_ms, float(errs), float(terminated)],
                          dtype=torch.float64, device=dev)
-    if world > 1:
-        tmax = stats[0:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        rest = stats[1:].clone()
-        dist.all_reduce(rest, op=dist.ReduceOp.SUM)
-        stats = torch.cat([tmax, rest])
-        # episode statistics gather (the only collective; RCCL all_gather, off the timed path)
-        mine = torch.tensor(counts1[:, [_abi.OC_NUM_COMPLETED, _abi.OC_NUM_ARRIVED, _abi.OC_DECISIONS]],
-                            dtype=torch.int32, device=dev)
-        gathered = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(gathered, mine)
+    stats = reduce_timing(stats, world)
+    # episode statistics gather (the only data collective; RCCL all_gather, off the timed path)
+    mine = torch.tensor(counts1[:, [_abi.OC_NUM_COMPLETED, _abi.OC_NUM_ARRIVED, _abi.OC_DECISIONS]],
+                        dtype=torch.int32, device=dev)
+    gathered = gather_env_stats(mine, world)
     elapsed, decisions, alg_bytes, kern_ms_sum, errs, terminated = stats.tolist()
     kern_ms = kern_ms_sum / world
     value = decisions / elapsed
     achieved = (alg_bytes / world / launches) / (kern_ms / launches / 1e3) / 1e9  # GB/s per GPU, dominant kernel
     kernel = "k_rollout" if args.mode == "rollout" else "k_step"
-    traffic, traffic_src = pmc_traffic(kernel, args.mode, B, decisions / world / launches)
+    traffic, traffic_src = pmc_traffic(kernel, args.mode, B, chunk if args.mode == "rollout" else 1,
+                                       decisions / world / launches)
     if rank == 0:
         line = {
             "metric": "scheduling decisions/sec (env steps/s)",
@@ -210,11 +210,13 @@ def main():
             "data": "synthetic TPC-H-format dataset (seeded generator), random valid actions (device RNG)",
             "config": {"workload": f"{B} envs/GPU x TPC-H 50 jobs / 10 executors (BASELINE configs[1])",
                        "envs_per_gpu": B, "jobs": 50, "executors": 10, "mode": args.mode,
-                       "steps_per_launch": args.chunk if args.mode == "rollout" else 1,
+                       "steps_per_launch": chunk if args.mode == "rollout" else 1,
                        "parallelism": f"env-sharded x{world}"},
             "decisions": int(decisions),
             "terminated_envs": int(terminated),
             "frozen_envs": int(errs),
+            "jobs_completed": int(gathered[:, 0].sum().item()),
+            "jobs_arrived": int(gathered[:, 1].sum().item()),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel,

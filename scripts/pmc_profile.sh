@@ -4,6 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 MODE=${PMC_MODE:-rollout}
+if [ "$MODE" = rollout ]; then ARGS="--steps 300 --warmup 50"; else ARGS="--steps 100 --warmup 20"; fi
 OUT=gpurun_out/pmc_$MODE
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -11,7 +12,7 @@ run() {
   local name=$1; shift
   echo "=== pmc $name ($(date +%T))"
   timeout -k 10 300 rocprofv3 --pmc "$@" -d "$PWD/$OUT/$name" -o run --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --mode "$MODE" --steps 100 --warmup 50 > "$OUT/$name.log" 2>&1
+    python3 bench.py --no-cpu-baseline --mode "$MODE" $ARGS > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   if [ $rc -ne 0 ]; then tail -n 20 "$OUT/$name.log"; exit $rc; fi
