@@ -32,6 +32,13 @@
 #define SSIM_TOC(v, ph) (void)0
 #endif
 
+// Diagnostic ISA-reading build only (-DSSIM_MARKERS): named asm comments delimit code regions in the .s output.
+#ifdef SSIM_MARKERS
+#define SSIM_MARK(name) asm volatile("; SSIM_MARK " name)
+#else
+#define SSIM_MARK(name) (void)0
+#endif
+
 namespace ssim {
 
 // Dataset pointers are loaded from the Params block, so the compiler sees generic pointers and would emit
@@ -922,7 +929,9 @@ struct Sim {
       double t;
       int kind, e, g, seq;
       SSIM_TIC(t_pop);
+      SSIM_MARK("pop_begin");
       const bool have = pop_event(&t, &kind, &e, &g, &seq);
+      SSIM_MARK("pop_end");
       SSIM_TOC(t_pop, kPhPop);
       if (!have) return false;
       SSIM_TIC(t_h);

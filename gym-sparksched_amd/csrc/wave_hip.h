@@ -50,20 +50,22 @@ struct WaveHip {
       const int y = __shfl_up(v, (unsigned)off);
       if (l >= off) v += y;
     }
-    *total = __shfl(v, 63);
+    *total = __builtin_amdgcn_readlane(v, 63);  // SGPR: the running total stays wave-uniform
     return v - x;
   }
   __device__ static __forceinline__ double sum_d(double x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-    return x;
+    return uni(x);
   }
   // Sparse argmins: the candidates are few (live commitments, pending executor events), so walk the
   // ballot of valid lanes with v_readlane instead of a 6-round ds_bpermute butterfly.
-  // lexicographic min of (key, val) over lanes with key != INT_MAX; result in every lane
+  // lexicographic min of (key, val) over lanes with key != INT_MAX; result in every lane (SGPRs: the
+  // accumulators start from constants, never from a lane's own value, so they stay wave-uniform).
+  // With no candidate, key = INT_MAX and val = -1.
   __device__ static __forceinline__ void min_pair(int& key, int& val) {
     uint64_t m = ballot(key != 0x7FFFFFFF);
-    int bk = 0x7FFFFFFF, bv = val;
+    int bk = 0x7FFFFFFF, bv = -1;
     while (m) {
       const int l = ffs(m);
       m &= m - 1;
@@ -79,7 +81,7 @@ struct WaveHip {
   // min of (t, seq) with payload idx over lanes with idx >= 0; result in every lane
   __device__ static __forceinline__ void min_event(double& t, int& seq, int& idx) {
     uint64_t m = ballot(idx >= 0);
-    double bt = t;
+    double bt = __builtin_inf();
     int bs = 0x7FFFFFFF, bi = -1;
     while (m) {
       const int l = ffs(m);
@@ -109,6 +111,6 @@ struct WaveHip {
       const int y = __shfl_xor(x, off);
       x = y > x ? y : x;
     }
-    return x;
+    return uni(x);
   }
 };
