@@ -875,31 +875,32 @@ struct Sim {
   }
 
   // Pops the min (t, seq) event: arrival cursor vs. per-executor slots. Returns false when empty.
+  // Each lane loads its executor's record; one wave argmin (W::argmin_event: DPP min of t, ties by seq)
+  // picks the winner, whose type / stage / seq are read from the winning lane's registers.
   __device__ __forceinline__ bool pop_event(double* t, int* kind, int* e, int* g, int* seq) {
+    constexpr int kSpan = W::kWidth < 16 ? W::kWidth : (kN > 0 && kN <= 16) ? 16 : 64;
     double bt = 0.0;
-    int bseq = 0x7FFFFFFF, be = -1;
-    for (int k0 = 0; k0 < NE; k0 += W::kWidth) {
+    int bseq = 0x7FFFFFFF, be = -1, btype = 0, bstage = -1;
+    const bool have_arr = h.arrivals < h.num_jobs;
+    const double ta = have_arr ? (double)job_tarr(h.arrivals) : 0.0;
+    for (int k0 = 0; k0 < NE; k0 += kSpan) {
       const int k = k0 + W::lane();
-      double tt = __builtin_inf();
-      int ss = 0x7FFFFFFF, kk = -1;
-      if (k < NE) {
-        const ExecRec r = exr(k);
-        if (r.ev_seq >= 0) {
-          tt = r.ev_t;
-          ss = r.ev_seq;
-          kk = k;
-        }
-      }
-      W::min_event(tt, ss, kk);
-      if (kk >= 0 && (be < 0 || tt < bt || (tt == bt && ss < bseq))) {
+      ExecRec r{};
+      r.ev_seq = -1;
+      if (k < NE && W::lane() < kSpan) r = exr(k);
+      double tt;
+      const int l = W::template argmin_event<kSpan>(r.ev_t, r.ev_seq, r.ev_seq >= 0, &tt);
+      if (l < 0) continue;
+      const int ss = W::bcast_i(r.ev_seq, l);
+      if (be < 0 || tt < bt || (tt == bt && ss < bseq)) {
         bt = tt;
         bseq = ss;
-        be = kk;
+        be = k0 + l;
+        btype = W::bcast_i(r.ev_type, l);
+        bstage = W::bcast_i(r.ev_stage, l);
       }
     }
-    const bool have_arr = h.arrivals < h.num_jobs;
     if (have_arr) {
-      const double ta = job_tarr(h.arrivals);
       const int sa = h.arrivals;  // arrivals were pushed first with seq 0..J-1
       if (be < 0 || ta < bt || (ta == bt && sa < bseq)) {
         *t = ta;
@@ -913,9 +914,9 @@ struct Sim {
     }
     if (be < 0) return false;
     *t = bt;
-    *kind = ev_type(be);
+    *kind = btype;
     *e = be;
-    *g = ev_stage(be);
+    *g = bstage;
     *seq = bseq;
     ev_seq(be) = -1;
     return true;
@@ -1003,6 +1004,17 @@ struct Sim {
     float* nodes = reinterpret_cast<float*>(obs + L.ob_nodes) + (int64_t)eid * SC * 3;
     uint8_t* front = obs + L.ob_frontier + (int64_t)eid * SC;
     int32_t* srank = reinterpret_cast<int32_t*>(obs + L.ob_sched_rank) + (int64_t)eid * SC;
+    // picks[j] (job id j): heuristics/utils.py find_stage of the job, packed as a min key over its
+    // schedulable nodes: (frontier ? 0 : 1 << 16) | schedulable rank; INT32_MAX = none. Nodes of a job are
+    // contiguous in node order and ranks grow with node order, so the min is the first frontier stage,
+    // else the first schedulable one.
+    int32_t* picks = H<int32_t>(O.picks);
+    const int16_t* ajl = H<int16_t>(O.active_jobs);
+    for (int k0 = 0; k0 < h.n_active_jobs; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      if (k < h.n_active_jobs) picks[ajl[k]] = 0x7FFFFFFF;
+    }
+    W::sync();
     int nsched = 0;
     for (int i0 = 0; i0 < n; i0 += W::kWidth) {
       const int i = i0 + W::lane();
@@ -1019,7 +1031,10 @@ struct Sim {
         front[i] = sr.unmet == 0 ? 1 : 0;
         srank[i] = s ? r : -1;
         row_of[g] = (int16_t)i;
-        if (s) sched[r] = (int16_t)g;
+        if (s) {
+          sched[r] = (int16_t)g;
+          W::amin(picks + sr.job, (sr.unmet == 0 ? 0 : 0x10000) | r);
+        }
       }
       nsched += W::popc(m);
     }
@@ -1084,6 +1099,7 @@ struct Sim {
     }
     if (ne > L.edge_cap) fail(SSIM_ERR_CAPACITY);
     h.n_sched = nsched;
+    h.src_idx = src_idx;
     h.stage_idx_n = n + 1;
     h.acc_nodes += n;
     h.acc_edges += ne;
@@ -1132,6 +1148,11 @@ struct Sim {
   // Requires the hot block in place (load_hot() by the caller for LDS residency).
   __device__ __forceinline__ void step(StepIn a) {
     load_header();
+    step_loaded(a);
+  }
+  __device__ __forceinline__ bool idle() const { return h.terminated || frozen() || h.num_jobs == 0; }
+  // step() with the header already in registers (the fused rollout loads it once for policy + step)
+  __device__ __forceinline__ void step_loaded(StepIn a) {
     if (h.terminated || frozen() || h.num_jobs == 0) return;
     SSIM_TIC(t_act);
     const int idx = a.stage_idx, nx = a.num_exec;

@@ -44,7 +44,8 @@ struct EnvHeader {
   int32_t episode;
   int32_t trace_len;
   int32_t step_events;
-  int32_t pad[3];
+  int32_t src_idx;        // obs source_job_idx at the last observation
+  int32_t pad[2];
   // running sums over observations (SURVEY.md §8d algorithmic-byte accounting)
   int64_t acc_nodes, acc_edges, acc_jobs, acc_events;
 };
@@ -120,7 +121,7 @@ struct StateOffsets {
   int64_t hot_bytes, cold_bytes, scratch_bytes, env_bytes;
   int64_t lds_bytes;        // scratch (+ hot when LDS-resident); decided by compute_layout
   int32_t lds_resident, pad;
-  int64_t hdr, jobs, jtimes, active_jobs, execs, sel_list, commits, stages, pools, active_stages, sched_list;
+  int64_t hdr, jobs, jtimes, active_jobs, picks, execs, sel_list, commits, stages, pools, active_stages, sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/;
   int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
       sc_row_of /*int16[S]*/;
@@ -149,6 +150,8 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   o = align16(o + (int64_t)sizeof(JobTimes) * J);
   O.active_jobs = o;
   o = align16(o + 2 * J);
+  O.picks = o;  // int32 [J]: per job id, heuristics find_stage at the last observation (packed, see observe)
+  o = align16(o + 4 * J);
   O.execs = o;
   o = align16(o + (int64_t)sizeof(ExecRec) * N);
   O.sel_list = o;

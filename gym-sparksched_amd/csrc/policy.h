@@ -26,6 +26,78 @@ __device__ __forceinline__ int uniform_below(uint64_t bits, int n) {
   return (int)(((bits & 0xFFFFFFFFULL) * (uint64_t)n) >> 32);
 }
 
+// The decision rule of the device policies over a per-active-job view (nj active jobs, index k in arrival
+// order): pick(k) = find_stage of job k (-1 = none), supply(k) = its exec supply; comm = committable
+// executors, src = source_job_idx. Shared by the obs-arena view (k_policy) and the fused rollout, which
+// passes the picks its observation pass computed (Sim::observe) so both give the same action.
+template <class W, class Pick, class Supply>
+__device__ __forceinline__ StepIn policy_act(int kind, uint64_t seed, uint64_t counter, int eid, int N, int nj,
+                                             int comm, int src, Pick pick, Supply supply) {
+  StepIn a;
+  a.stage_idx = -1;
+  a.num_exec = comm > 0 ? comm : 1;
+  if (kind == SSIM_POLICY_FAIR || kind == SSIM_POLICY_FIFO) {
+    const int cap = kind == SSIM_POLICY_FAIR ? (N + (nj > 1 ? nj : 1) - 1) / (nj > 1 ? nj : 1) : N;
+    if (src < nj) {
+      const int s = W::uni(pick(src));
+      if (s >= 0) {
+        a.stage_idx = s;
+        return a;
+      }
+    }
+    for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      const bool ok = k < nj && k != src && supply(k) < cap;
+      const int s = ok ? pick(k) : -1;
+      const uint64_t m = W::ballot(s >= 0);
+      if (m) {
+        const int l = W::ffs(m);
+        a.stage_idx = W::bcast_i(s, l);
+        const int room = cap - W::bcast_i(ok ? supply(k) : 0, l);
+        a.num_exec = comm < room ? comm : room;
+        return a;
+      }
+    }
+    return a;
+  }
+  // RANDOM
+  const uint64_t key = splitmix64(seed ^ splitmix64((uint64_t)eid * 0xD1B54A32D192ED03ULL + counter));
+  if (nj <= W::kWidth) {  // one chunk: each lane keeps its job's pick
+    const int k = W::lane();
+    const int s = k < nj ? pick(k) : -1;
+    const uint64_t m = W::ballot(s >= 0);
+    const int valid = W::popc(m);
+    if (valid > 0) {
+      const int r = uniform_below(splitmix64(key ^ 0x1ULL), valid);
+      const int l = W::ffs(W::ballot(s >= 0 && W::rank(m) == r));
+      a.stage_idx = W::bcast_i(s, l);
+    }
+  } else {
+    int valid = 0;
+    for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      valid += W::popc(W::ballot(k < nj && pick(k) >= 0));
+    }
+    if (valid > 0) {
+      int r = uniform_below(splitmix64(key ^ 0x1ULL), valid);
+      for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
+        const int k = k0 + W::lane();
+        const int s = k < nj ? pick(k) : -1;
+        const uint64_t m = W::ballot(s >= 0);
+        const int cnt = W::popc(m);
+        if (r < cnt) {
+          const int l = W::ffs(W::ballot(s >= 0 && W::rank(m) == r));
+          a.stage_idx = W::bcast_i(s, l);
+          break;
+        }
+        r -= cnt;
+      }
+    }
+  }
+  a.num_exec = comm > 0 ? 1 + uniform_below(splitmix64(key ^ 0x2ULL), comm) : 1;
+  return a;
+}
+
 template <class W>
 struct PolicyView {
   const ssim_layout& L;
@@ -63,63 +135,27 @@ struct PolicyView {
 
   __device__ __forceinline__ StepIn act(int kind, uint64_t seed, uint64_t counter) const {
     const int32_t* c = counts();
-    const int nj = c[SSIM_OC_NUM_JOBS], comm = c[SSIM_OC_COMMITTABLE], src = c[SSIM_OC_SOURCE_JOB_IDX];
-    const int N = L.num_executors;
-    StepIn a;
-    a.stage_idx = -1;
-    a.num_exec = comm > 0 ? comm : 1;
-    if (kind == SSIM_POLICY_FAIR || kind == SSIM_POLICY_FIFO) {
-      const int cap = kind == SSIM_POLICY_FAIR ? (N + (nj > 1 ? nj : 1) - 1) / (nj > 1 ? nj : 1) : N;
-      if (src < nj) {
-        const int s = find_stage(src);
-        if (s >= 0) {
-          a.stage_idx = s;
-          return a;
-        }
-      }
-      const int32_t* su = sup();
-      for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
-        const int k = k0 + W::lane();
-        const bool ok = k < nj && su[k] < cap && k != src;
-        const int s = ok ? find_stage(k) : -1;
-        const uint64_t m = W::ballot(s >= 0);
-        if (m) {
-          const int l = W::ffs(m);
-          const int kk = k0 + l;
-          a.stage_idx = W::bcast_i(s, l);
-          const int room = cap - su[kk];
-          a.num_exec = comm < room ? comm : room;
-          return a;
-        }
-      }
-      return a;
-    }
-    // RANDOM
-    const uint64_t key = splitmix64(seed ^ splitmix64((uint64_t)eid * 0xD1B54A32D192ED03ULL + counter));
-    int valid = 0;
-    for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
-      const int k = k0 + W::lane();
-      valid += W::popc(W::ballot(k < nj && find_stage(k) >= 0));
-    }
-    if (valid > 0) {
-      int r = uniform_below(splitmix64(key ^ 0x1ULL), valid);
-      for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
-        const int k = k0 + W::lane();
-        const int s = k < nj ? find_stage(k) : -1;
-        const uint64_t m = W::ballot(s >= 0);
-        const int cnt = W::popc(m);
-        if (r < cnt) {
-          const bool mine = s >= 0 && W::rank(m) == r;
-          const int l = W::ffs(W::ballot(mine));
-          a.stage_idx = W::bcast_i(s, l);
-          break;
-        }
-        r -= cnt;
-      }
-    }
-    a.num_exec = comm > 0 ? 1 + uniform_below(splitmix64(key ^ 0x2ULL), comm) : 1;
-    return a;
+    const int32_t* su = sup();
+    return policy_act<W>(kind, seed, counter, eid, L.num_executors, c[SSIM_OC_NUM_JOBS], c[SSIM_OC_COMMITTABLE],
+                         c[SSIM_OC_SOURCE_JOB_IDX], [&](int k) { return find_stage(k); },
+                         [&](int k) { return su[k]; });
   }
 };
+
+// The fused rollout's policy input: the header (loaded) and the picks of the env's last observation
+// (Sim::observe), read from the hot block instead of the obs arena the same wave just wrote.
+template <class W, int kN, int kJ>
+__device__ __forceinline__ StepIn sim_policy(Sim<W, kN, kJ>& s, int kind, uint64_t seed) {
+  const int16_t* aj = s.template H<int16_t>(s.O.active_jobs);
+  const int32_t* picks = s.template H<int32_t>(s.O.picks);
+  const uint64_t counter = (uint64_t)s.h.decisions + ((uint64_t)s.h.episode << 32);
+  return policy_act<W>(
+      kind, seed, counter, s.eid, s.NE, s.h.n_active_jobs, s.committable(), s.h.src_idx,
+      [&](int k) {
+        const int key = picks[aj[k]];
+        return key == 0x7FFFFFFF ? -1 : (key & 0xFFFF);
+      },
+      [&](int k) { return (int)s.job(aj[k]).supply; });
+}
 
 }  // namespace ssim

@@ -74,14 +74,13 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
   const int B = P->L.num_envs;
   if (env_idle(P, state, eid) && action_log == nullptr) return;
   Sim<WaveHip, kN, kJ> s(P, state, g_smem, obs, eid, kRes);
-  PolicyView<WaveHip> v{P->L, obs, eid};
   s.load_hot();
-  const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.hot + P->O.hdr);
   for (int k = 0; k < num_steps; ++k) {
 #ifdef SSIM_PROFILE
     const uint64_t t0 = WaveHip::clock();
 #endif
-    const StepIn a = v.act(kind, seed, (uint64_t)hd->decisions + ((uint64_t)hd->episode << 32));
+    s.load_header();
+    const StepIn a = sim_policy(s, kind, seed);
 #ifdef SSIM_PROFILE
     s.prof[kPhPolicy] += WaveHip::clock() - t0;
 #endif
@@ -90,7 +89,7 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
       action_log[((int64_t)k * B + eid) * 2 + 1] = a.num_exec;
     }
     WaveHip::sync();
-    s.step(a);
+    s.step_loaded(a);
   }
   s.save_hot();
 #ifdef SSIM_PROFILE

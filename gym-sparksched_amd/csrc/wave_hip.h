@@ -78,25 +78,55 @@ struct WaveHip {
     key = bk;
     val = bv;
   }
-  // min of (t, seq) with payload idx over lanes with idx >= 0; result in every lane
-  __device__ static __forceinline__ void min_event(double& t, int& seq, int& idx) {
-    uint64_t m = ballot(idx >= 0);
-    double bt = __builtin_inf();
-    int bs = 0x7FFFFFFF, bi = -1;
-    while (m) {
-      const int l = ffs(m);
-      m &= m - 1;
-      const double t2 = bcast_d(t, l);
-      const int s2 = bcast_i(seq, l);
-      if (bi < 0 || t2 < bt || (t2 == bt && s2 < bs)) {
-        bt = t2;
-        bs = s2;
-        bi = bcast_i(idx, l);
+  // Wave min of a double over lanes [0, kSpan) (kSpan 16 or 64), wave-uniform result. Row stages are DPP
+  // (quad xor 1, xor 2, row_ror 4, row_ror 8: every lane of a row ends with the row min), then for a full
+  // wave the four row minima are combined on the scalar side. All 64 lanes must be active (callers run in
+  // wave-uniform control flow).
+  template <int kCtrl>
+  __device__ static __forceinline__ double dpp_d(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)b, (int)(uint32_t)b, kCtrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(b >> 32), (int)(uint32_t)(b >> 32), kCtrl, 0xF, 0xF,
+                                               false);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
+  template <int kSpan>
+  __device__ static __forceinline__ double min_d(double v) {
+    v = __builtin_fmin(v, dpp_d<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = __builtin_fmin(v, dpp_d<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = __builtin_fmin(v, dpp_d<0x124>(v));  // row_ror:4
+    v = __builtin_fmin(v, dpp_d<0x128>(v));  // row_ror:8
+    double m = bcast_d(v, 0);
+    if (kSpan > 16) {
+      const double m1 = bcast_d(v, 16), m2 = bcast_d(v, 32), m3 = bcast_d(v, 48);
+      m = __builtin_fmin(__builtin_fmin(m, m1), __builtin_fmin(m2, m3));
+      m = uni(m);
+    }
+    return m;
+  }
+  // Argmin of (t, seq) over lanes [0, kSpan) with `valid`: the winning lane (-1 if none). One DPP min of t,
+  // then the (rare) ties on t are broken by the smaller seq. `tmin` receives the winning t.
+  template <int kSpan>
+  __device__ static __forceinline__ int argmin_event(double t, int seq, bool valid, double* tmin) {
+    const double m = min_d<kSpan>(valid ? t : __builtin_inf());
+    uint64_t eq = ballot(valid && t == m);
+    *tmin = m;
+    if (eq == 0) return -1;
+    int l = ffs(eq);
+    eq &= eq - 1;
+    if (eq) {
+      int bs = bcast_i(seq, l);
+      while (eq) {
+        const int l2 = ffs(eq);
+        eq &= eq - 1;
+        const int s2 = bcast_i(seq, l2);
+        if (s2 < bs) {
+          bs = s2;
+          l = l2;
+        }
       }
     }
-    t = bt;
-    seq = bs;
-    idx = bi;
+    return l;
   }
   // correctly rounded f32 ops (the reference's numpy float32 arithmetic; no contraction)
   __device__ static __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
@@ -104,6 +134,7 @@ struct WaveHip {
   // LDS atomics / loads for lane-parallel relaxations
   __device__ static __forceinline__ int lds_load(const int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
   __device__ static __forceinline__ void amax(int* p, int v) { atomicMax(p, v); }
+  __device__ static __forceinline__ void amin(int* p, int v) { atomicMin(p, v); }
   __device__ static __forceinline__ void aor(uint32_t* p, uint32_t v) { atomicOr(p, v); }
   __device__ static __forceinline__ int max_i(int x) {
 #pragma unroll

@@ -118,7 +118,9 @@ class HostEngine:
 
     def rollout(self, kind, seed, num_steps, action_log=None):
         ptr = action_log.ctypes.data if action_log is not None else None
-        lib().hs_rollout(self.handle, kind, seed, num_steps, ptr)
+        rc = lib().hs_rollout(self.handle, kind, seed, num_steps, ptr)
+        assert rc == 0, "hostsim rollout: the hot-block policy view disagreed with the obs-arena view" if rc == -5 \
+            else f"hostsim rollout rc={rc}"
 
     def host_views(self):
         return self.views

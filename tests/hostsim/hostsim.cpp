@@ -44,10 +44,15 @@ struct WaveSerial {
   static float fmul(float a, float b) { return a * b; }
   static int lds_load(const int* p) { return *p; }
   static void amax(int* p, int v) { *p = v > *p ? v : *p; }
+  static void amin(int* p, int v) { *p = v < *p ? v : *p; }
   static void aor(uint32_t* p, uint32_t v) { *p |= v; }
   static int max_i(int x) { return x; }
   static void min_pair(int&, int&) {}
-  static void min_event(double&, int&, int&) {}
+  template <int kSpan>
+  static int argmin_event(double t, int, bool valid, double* tmin) {
+    *tmin = valid ? t : __builtin_inf();
+    return valid ? 0 : -1;
+  }
 };
 
 struct hs_handle {
@@ -132,13 +137,16 @@ int hs_rollout(hs_handle* h, int kind, uint64_t seed, int num_steps, int32_t* ac
     Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
     PolicyView<WaveSerial> v{P->L, h->obs, e};
     for (int k = 0; k < num_steps; ++k) {
-      const EnvHeader* hd = reinterpret_cast<const EnvHeader*>(s.hot + P->O.hdr);
-      const StepIn a = v.act(kind, seed, (uint64_t)hd->decisions + ((uint64_t)hd->episode << 32));
+      // the device rollout's policy (picks from the hot block) must equal the obs-arena view's (k_policy)
+      s.load_header();
+      const StepIn a = sim_policy(s, kind, seed);
+      const StepIn b = v.act(kind, seed, (uint64_t)s.h.decisions + ((uint64_t)s.h.episode << 32));
+      if (!s.idle() && (a.stage_idx != b.stage_idx || a.num_exec != b.num_exec)) return -5;
       if (action_log) {
         action_log[((int64_t)k * B + e) * 2 + 0] = a.stage_idx;
         action_log[((int64_t)k * B + e) * 2 + 1] = a.num_exec;
       }
-      s.step(a);
+      s.step_loaded(a);
     }
   }
   return 0;
