@@ -55,7 +55,14 @@ __device__ __forceinline__ T ldg(const T* p, int64_t i) {
 
 // top-level phases (disjoint) then inclusive sub-timers (nested inside the top-level ones)
 enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kPhHandle, kPhPostScan, kPhObserve,
-                 kPhSample, kPhPool, kPhScan, kPhLoadSave, kNumPhases };
+                 kPhSample, kPhPool, kPhScan, kPhLoadSave, kPhPoolBig, kPhIdleOrder, kPhDraw,
+                 // event counters (not cycles)
+                 kCtPoolSmall, kCtPoolBig, kCtTask, kCtIdleOrder, kNumPhases };
+#ifdef SSIM_PROFILE
+#define SSIM_COUNT(ph) prof[ph] += 1
+#else
+#define SSIM_COUNT(ph) (void)0
+#endif
 enum : int32_t { kPoolNone = -1, kPoolCommon = 0 };
 enum : int32_t { kEvArrival = 1, kEvTask = 2, kEvReady = 3, kTrJobDone = 4 };
 enum : int32_t { kJobPending = 0, kJobActive = 1, kJobDone = 2 };
@@ -416,11 +423,17 @@ struct Sim {
     const int size = (int)W::uni(pool(p).mask) + 1;
     W::sync();
     if (size == 8) {
+      SSIM_COUNT(kCtPoolSmall);
       const uint8_t* g = pool(p).tab;
       for (int i = W::lane(); i < 8; i += W::kWidth) t[i] = g[i];
     } else {
+      SSIM_COUNT(kCtPoolBig);
+      SSIM_TIC(t0);
       const uint8_t* g = ptab(p);
       for (int i = W::lane(); i < size; i += W::kWidth) t[i] = g[i];
+      W::sync();
+      if (W::uni(t[0]) == 0xFD) t[0] = 0xFD;  // profile build only: wait for the staged bytes
+      SSIM_TOC(t0, kPhPoolBig);
     }
     W::sync();
     return t;
@@ -437,8 +450,197 @@ struct Sim {
     }
     W::sync();
   }
+  // ---- lane-parallel CPython-set operations (device waves; tables of <= 64 slots, i.e. N <= 15) ----
+  // Lane i holds slot i of the table. The probe sequence of pyset.h is walked on wave-uniform 64-bit
+  // ballots (EMPTY / DUMMY / key slots) with SALU bit operations, so an operation costs one lane-parallel
+  // table load instead of a chain of dependent single-byte reads. Same semantics as pyset.h (whose serial
+  // form the host build keeps, pinned against CPython by tests/test_kats.py); the device form is pinned by
+  // the GPU parity tests' per-event executor traces.
+  static constexpr bool kLaneSets = W::kWidth == 64;
+  __device__ __forceinline__ bool lane_sets() const { return kLaneSets && set_cap_for(NE) <= 64; }
+  __device__ __forceinline__ static uint64_t slot_bits(uint32_t mask) {
+    return mask >= 63 ? ~0ull : ((1ull << (mask + 1)) - 1);
+  }
+  // CPython probe walk for `key` over the ballots: returns the slot holding key or -1; *empty = the EMPTY
+  // slot that ended the walk, *dummy = the last DUMMY slot seen before it (-1: none) — set_add_entry's
+  // freeslot. Tables without dummies and without the key give set_insert_clean's slot in *empty.
+  __device__ __forceinline__ static int lt_probe(uint64_t E, uint64_t Dm, uint64_t K, uint32_t mask, uint32_t key,
+                                                 int* empty, int* dummy) {
+    uint32_t i = key & mask, perturb = key;
+    int fd = -1;
+    for (;;) {
+      const uint64_t w = (i + 9u <= mask) ? (0x3FFull << i) : (1ull << i);
+      const uint64_t stop = (E | K) & w;
+      if (stop) {
+        const int f = __builtin_ctzll(stop);
+        const uint64_t d = Dm & w & ((1ull << f) - 1);
+        if (d) fd = 63 - __builtin_clzll(d);
+        *dummy = fd;
+        if ((K >> f) & 1ull) {
+          *empty = -1;
+          return f;
+        }
+        *empty = f;
+        return -1;
+      }
+      const uint64_t d = Dm & w;
+      if (d) fd = 63 - __builtin_clzll(d);
+      perturb >>= 5;
+      i = (i * 5u + 1u + perturb) & mask;
+    }
+  }
+  __device__ __forceinline__ int lt_load(int p, uint32_t mask) {  // this lane's slot byte (EMPTY past the table)
+    const int l = W::lane();
+    int v = kSlotEmpty;
+    if (mask == 7) {
+      if (l < 8) v = pool(p).tab[l];
+    } else {
+      if (l <= (int)mask) v = ptab(p)[l];
+    }
+    return v;
+  }
+  __device__ __forceinline__ void lt_store(int p, uint32_t mask, int slot, int val) {
+    W::sync();
+    if (W::lane() == 0) {
+      if (mask == 7)
+        pool(p).tab[slot] = (uint8_t)val;
+      else
+        ptab(p)[slot] = (uint8_t)val;
+    }
+    W::sync();
+  }
+  __device__ __forceinline__ void lt_meta(int p, uint32_t mask, uint32_t fill, uint32_t used) {
+    W::sync();
+    if (W::lane() == 0) {
+      PoolRec& r = pool(p);
+      r.mask = (uint16_t)mask;
+      r.fill = (uint16_t)fill;
+      r.used = (uint16_t)used;
+    }
+    W::sync();
+  }
+  // Clean insert of the slot values of `v` (occupied slots in `occ`, table order) into a fresh table of
+  // `size` slots; returns the new table (this lane's slot).
+  __device__ __forceinline__ static int lt_reinsert(int v, uint64_t occ, uint32_t size) {
+    const uint32_t mask = size - 1;
+    uint64_t E = slot_bits(mask);
+    int nv = kSlotEmpty;
+    while (occ) {
+      const int s = __builtin_ctzll(occ);
+      occ &= occ - 1;
+      const int key = W::bcast_i(v, s);
+      int slot, dm;
+      lt_probe(E, 0, 0, mask, (uint32_t)key, &slot, &dm);
+      E &= ~(1ull << slot);
+      nv = W::writelane(key, slot, nv);
+    }
+    return nv;
+  }
+  // set_table_resize(minused) of pool p whose current slots are `v`; writes the table to its new home.
+  __device__ __forceinline__ void lt_resize(int p, int v, uint32_t mask, uint32_t minused) {
+    const uint64_t occ = W::ballot(v < kSlotDummy) & slot_bits(mask);
+    const uint32_t n = (uint32_t)W::popc(occ);
+    uint32_t size = 8;
+    while (size <= minused) size <<= 1;
+    const int nv = lt_reinsert(v, occ, size);
+    const int l = W::lane();
+    if (size == 8) {
+      if (l < 8) pool(p).tab[l] = (uint8_t)nv;
+    } else {
+      if (l < (int)size) ptab(p)[l] = (uint8_t)nv;
+    }
+    lt_meta(p, size - 1, n, n);
+  }
+  __device__ __forceinline__ void pool_add_lanes(int p, int e) {
+    const uint32_t mask = W::uni(pool(p).mask), fill = W::uni(pool(p).fill), used = W::uni(pool(p).used);
+    const int v = lt_load(p, mask);
+    const uint64_t E = W::ballot(v == kSlotEmpty) & slot_bits(mask), Dm = W::ballot(v == kSlotDummy),
+                   K = W::ballot(v == e);
+    int empty, dummy;
+    if (lt_probe(E, Dm, K, mask, (uint32_t)e, &empty, &dummy) >= 0) return;  // already present
+    if (dummy >= 0) {
+      lt_store(p, mask, dummy, e);
+      lt_meta(p, mask, fill, used + 1);
+      return;
+    }
+    if ((fill + 1) * 5u >= mask * 3u) {
+      lt_resize(p, W::lane() == empty ? e : v, mask, (used + 1) * 4);
+      return;
+    }
+    lt_store(p, mask, empty, e);
+    lt_meta(p, mask, fill + 1, used + 1);
+  }
+  __device__ __forceinline__ bool pool_remove_lanes(int p, int e) {
+    const uint32_t mask = W::uni(pool(p).mask), fill = W::uni(pool(p).fill), used = W::uni(pool(p).used);
+    const int v = lt_load(p, mask);
+    const uint64_t E = W::ballot(v == kSlotEmpty) & slot_bits(mask), K = W::ballot(v == e);
+    int empty, dummy;
+    const int slot = lt_probe(E, 0, K, mask, (uint32_t)e, &empty, &dummy);
+    if (slot < 0) return false;
+    lt_store(p, mask, slot, kSlotDummy);
+    lt_meta(p, mask, fill, used - 1);
+    return true;
+  }
+  // Keys (lane r = r-th key) in the iteration order of set(keys) built by sequential adds into a fresh set.
+  __device__ __forceinline__ static int lt_build_order(int kv, int n) {
+    uint32_t mask = 7, fill = 0;
+    uint64_t E = 0xFFull;
+    int tv = kSlotEmpty;
+    for (int r = 0; r < n; ++r) {
+      const int key = W::bcast_i(kv, r);
+      int slot, dm;
+      lt_probe(E, 0, 0, mask, (uint32_t)key, &slot, &dm);
+      E &= ~(1ull << slot);
+      tv = W::writelane(key, slot, tv);
+      fill++;
+      if (fill * 5u >= mask * 3u) {  // ps_resize(used * 4): clean re-insert in table order
+        uint32_t size = 8;
+        while (size <= fill * 4u) size <<= 1;
+        const uint64_t occ = ~E & slot_bits(mask);
+        tv = lt_reinsert(tv, occ, size);
+        mask = size - 1;
+        E = W::ballot(tv == kSlotEmpty) & slot_bits(mask);
+      }
+    }
+    return W::compact(~E & slot_bits(mask), tv);
+  }
+  // idle_order (below) for lane-sized tables: out[0..n) = executor ids, returns n.
+  __device__ __forceinline__ int idle_order_lanes(int p, int32_t* out) {
+    const uint32_t mask = W::uni(pool(p).mask), fill = W::uni(pool(p).fill), used = W::uni(pool(p).used);
+    const int v = lt_load(p, mask);
+    const uint64_t occ = W::ballot(v < kSlotDummy) & slot_bits(mask);
+    int n = W::popc(occ);
+    int kv = W::compact(occ, v);  // keys in table order
+    // pool.copy(): same order if the fresh table has the same mask and the source no dummies
+    uint32_t size = 8;
+    if (n * 5 >= 21)
+      while ((int)size <= n * 2) size <<= 1;
+    if (n > 0 && !(size - 1 == mask && fill == used)) {
+      const int tv = lt_reinsert(kv, (n >= 64 ? ~0ull : ((1ull << n) - 1)), size);
+      kv = W::compact(W::ballot(tv != kSlotEmpty) & slot_bits(size - 1), tv);
+    }
+    // filter `not executor.is_executing`, keeping order
+    const int l = W::lane();
+    const bool keep = l < n && !exr(l < n ? kv : 0).busy;
+    const uint64_t mk = W::ballot(keep);
+    kv = W::compact(mk, kv);
+    n = W::popc(mk);
+    kv = lt_build_order(kv, n);
+    W::sync();
+    if (l < n) out[l] = kv;
+    W::sync();
+    return n;
+  }
+
   __device__ __forceinline__ void pool_add(int p, int e) {
     SSIM_TIC(t0);
+    if constexpr (kLaneSets) {
+      if (lane_sets()) {
+        pool_add_lanes(p, e);
+        SSIM_TOC(t0, kPhPool);
+        return;
+      }
+    }
     uint8_t* t = stage_table(p);
     ps_add<W>(pmeta(p), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));
     unstage_table(p, t);
@@ -446,6 +648,13 @@ struct Sim {
   }
   __device__ __forceinline__ void pool_remove(int p, int e) {
     SSIM_TIC(t0);
+    if constexpr (kLaneSets) {
+      if (lane_sets()) {
+        check(pool_remove_lanes(p, e));
+        SSIM_TOC(t0, kPhPool);
+        return;
+      }
+    }
     uint8_t* t = stage_table(p);
     const bool ok = ps_remove<W>(pmeta(p), t, (uint32_t)e);
     unstage_table(p, t);
@@ -479,7 +688,16 @@ struct Sim {
   // Table order of set(e for e in pool.copy() if not busy) — _get_idle_source_executors (:714-728).
   __device__ __forceinline__ int idle_order(int p, int32_t* out) {
     if (p < 0) return 0;
+    SSIM_COUNT(kCtIdleOrder);
     SSIM_TIC(t0);
+    if constexpr (kLaneSets) {
+      if (lane_sets()) {
+        const int n = idle_order_lanes(p, out);
+        SSIM_TOC(t0, kPhPool);
+        SSIM_TOC(t0, kPhIdleOrder);
+        return n;
+      }
+    }
     const uint8_t* t = stage_table(p);
     const PySetMeta* m = pmeta(p);
     int n = ps_keys<W>(m, t, out);
@@ -493,6 +711,7 @@ struct Sim {
     ps_build_order<W>(out, n, S<uint8_t>(O.sc_tab_b), S<int32_t>(O.sc_keys_b));
     W::sync();
     SSIM_TOC(t0, kPhPool);
+    SSIM_TOC(t0, kPhIdleOrder);
     return n;
   }
 
@@ -549,8 +768,10 @@ struct Sim {
       off = ldu(D.dur_off, idx);
     }
     if (len <= 0) return false;  // KeyError (missing) or ValueError (empty): no RNG consumed
+    SSIM_TIC(t0);
     const uint32_t k = rng.bounded((uint32_t)len);
     *out = ldu(D.durations, off + (int)k);
+    SSIM_TOC(t0, kPhDraw);
     return true;
   }
 
@@ -676,6 +897,7 @@ struct Sim {
     st_exe(g) += 1;
     if (st_rem(g) == 0) job_sat(j) += 1;
     SSIM_TIC(t_smp);
+    SSIM_COUNT(kCtTask);
     const double dur = task_duration(j, g, e);
     SSIM_TOC(t_smp, kPhSample);
     ex_task(e) = (int16_t)(g - job_base(j));

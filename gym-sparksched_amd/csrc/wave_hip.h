@@ -128,6 +128,15 @@ struct WaveHip {
     }
     return l;
   }
+  // wave-uniform value into lane `l` of a per-lane value (`l` wave-uniform)
+  __device__ static __forceinline__ int writelane(int v, int l, int old) { return lane() == l ? v : old; }
+  // Forward permute: this lane's v goes to lane `dst` (a permutation of the lanes; ds_permute_b32)
+  __device__ static __forceinline__ int permute_to(int dst, int v) { return __builtin_amdgcn_ds_permute(dst << 2, v); }
+  // Compaction keeping lane order: lanes in `m` move to lanes 0..popc(m)-1, the rest after them
+  __device__ static __forceinline__ int compact(uint64_t m, int v) {
+    const bool in = (m >> lane()) & 1ull;
+    return permute_to(in ? rank(m) : popc(m) + rank(~m), v);
+  }
   // correctly rounded f32 ops (the reference's numpy float32 arithmetic; no contraction)
   __device__ static __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
   __device__ static __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }

@@ -33,6 +33,8 @@ struct WaveSerial {
     return v;
   }
   static int bcast_i(int v, int) { return v; }
+  static int writelane(int v, int, int) { return v; }
+  static int compact(uint64_t, int v) { return v; }
   static void sync() {}
   static uint64_t clock() { return 0; }
   static int excl_scan(int x, int* total) {
