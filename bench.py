@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-autoreset", action="store_true",
+                    help="rollout mode: leave finished envs idle instead of resetting them on the device")
     args = ap.parse_args()
 
     import numpy as np
@@ -129,6 +131,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     chunk = args.chunk if args.chunk > 0 else K
+    flags = 0 if args.no_autoreset else _abi.SSIM_ROLLOUT_AUTORESET
 
     def chunks(n):
         return [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
@@ -138,7 +141,7 @@ def main():
             for k, c in enumerate(chunks(n)):
                 if events is not None:
                     events[2 * k].record(stream)
-                eng.rollout(kind, 1234, c)
+                eng.rollout(kind, 1234, c, flags=flags)
                 if events is not None:
                     events[2 * k + 1].record(stream)
         else:
@@ -173,9 +176,10 @@ def main():
     counts1 = eng.views["counts"].cpu().numpy()
     acc1 = eng.views["acc"].cpu().numpy()
     errs = int(np.count_nonzero(counts1[:, _abi.OC_ERR] & _abi.SSIM_ERR_STICKY))
-    decisions = int((counts1[:, _abi.OC_DECISIONS] - counts0[:, _abi.OC_DECISIONS]).sum())
+    d_acc = (acc1 - acc0).sum(axis=0).astype(np.float64)  # S_act, E_act, J_act, events, decisions, episodes
+    decisions = int(d_acc[_abi.ACC_DECISIONS])  # over all episodes (auto-reset restarts the per-episode count)
     terminated = int(counts1[:, _abi.OC_TERMINATED].sum())
-    d_acc = (acc1 - acc0).sum(axis=0).astype(np.float64)  # S_act, E_act, J_act, events
+    episodes_done = int(d_acc[_abi.ACC_EPISODES])
     # B_dec = 36 S_act + 20 E_act + 16 J_act + 96 K + 40 bytes per decision
     alg_bytes = 36 * d_acc[0] + 20 * d_acc[1] + 16 * d_acc[2] + 96 * d_acc[3] + 40 * decisions
     kern_ms = sum(events[2 * k].elapsed_time(events[2 * k + 1]) for k in range(launches))
@@ -211,9 +215,11 @@ def main():
             "config": {"workload": f"{B} envs/GPU x TPC-H 50 jobs / 10 executors (BASELINE configs[1])",
                        "envs_per_gpu": B, "jobs": 50, "executors": 10, "mode": args.mode,
                        "steps_per_launch": chunk if args.mode == "rollout" else 1,
+                       "autoreset": bool(args.mode == "rollout" and flags),
                        "parallelism": f"env-sharded x{world}"},
             "decisions": int(decisions),
             "terminated_envs": int(terminated),
+            "episodes_finished": episodes_done,
             "frozen_envs": int(errs),
             "jobs_completed": int(gathered[:, 0].sum().item()),
             "jobs_arrived": int(gathered[:, 1].sum().item()),

@@ -1329,11 +1329,15 @@ struct Sim {
     h.acc_events += h.step_events;
     W::sync();
     if (W::lane() == 0) {
-      int64_t* acc = reinterpret_cast<int64_t*>(obs + L.ob_acc) + (int64_t)eid * 4;
+      int64_t* acc = reinterpret_cast<int64_t*>(obs + L.ob_acc) + (int64_t)eid * kNumAcc;
       acc[0] = h.acc_nodes;
       acc[1] = h.acc_edges;
       acc[2] = h.acc_jobs;
       acc[3] = h.acc_events;
+      acc[4] = h.acc_decisions;
+      acc[5] = h.acc_episodes;
+      acc[6] = 0;
+      acc[7] = 0;
       int32_t* cnts = reinterpret_cast<int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
       cnts[SSIM_OC_NUM_NODES] = n;
       cnts[SSIM_OC_NUM_EDGES] = ne;
@@ -1409,6 +1413,7 @@ struct Sim {
       W::sync();
     }
     h.decisions++;
+    h.acc_decisions++;
     h.step_events = 0;
     SSIM_TOC(t_act, kPhAction);
     SSIM_TIC(t_rc);
@@ -1448,6 +1453,60 @@ struct Sim {
     store_header();
   }
 
+  // ---------------------------------------------------------------- device-side reset sampling
+  // TPCHDataSampler.job_sequence (tpch.py:54-73) on the env's RNG `rng`: per job integers(22) + 1 (query),
+  // choice(QUERY_SIZES) (= integers(0, 7)), arrival t, then t += exponential(1 / rate) (drawn after every
+  // job, the last included), while t < time_limit and under the arrival cap. Writes the arrival times and
+  // template ids of the env's reset record (HBM, lane 0) and returns the job count (-1: over job_cap).
+  __device__ __forceinline__ int sample_job_sequence(double time_limit, uint8_t* rec_base) {
+    double* tarr = reinterpret_cast<double*>(rec_base + kResetHeadBytes);
+    int32_t* tpl = reinterpret_cast<int32_t*>(rec_base + kResetHeadBytes + 8 * (int64_t)JC);
+    const int cap = C.job_arrival_cap;
+    double t = 0.0;
+    int k = 0;
+    while (t < time_limit && (cap == 0 || k < cap)) {
+      if (k >= JC) return -1;
+      const int q = 1 + (int)rng.bounded(22);
+      const int sz = (int)rng.bounded(7);
+      if (W::lane() == 0) {
+        tpl[k] = (q - 1) * 7 + sz;
+        tarr[k] = t;
+      }
+      t += C.job_arrival_gap * rng.std_exponential();
+      k++;
+    }
+    return k;
+  }
+
+  // reset(seed=None | seed) with the job sequence sampled on the device; then reset() from the record.
+  // `mode`: SSIM_RESET_CONTINUE continues the env's current stream (header loaded), SSIM_RESET_SEED
+  // reseeds it as Generator(PCG64(SeedSequence(seed))).
+  __device__ __forceinline__ void reset_sampled(int mode, uint64_t seed, double time_limit, uint8_t* rec_base) {
+    if (mode == SSIM_RESET_SEED) {
+      rng = Pcg64::from_seed(seed);
+    } else if (h.num_jobs == 0 && h.episode == 0) {  // no stream to continue: never reset before
+      fail(SSIM_ERR_RESET);
+      store_header();
+      return;
+    }
+    int n = 0;
+    if (!(time_limit == __builtin_inf() && C.job_arrival_cap == 0) && C.job_arrival_gap > 0.0)
+      n = sample_job_sequence(time_limit, rec_base);
+    ssim_reset_record* rec = reinterpret_cast<ssim_reset_record*>(rec_base);
+    if (W::lane() == 0) {
+      rec->rng_state_hi = rng.s_hi;
+      rec->rng_state_lo = rng.s_lo;
+      rec->rng_inc_hi = rng.i_hi;
+      rec->rng_inc_lo = rng.i_lo;
+      rec->rng_has_uint32 = rng.has32;
+      rec->rng_uinteger = rng.u32;
+      rec->num_jobs = n > 0 ? n : JC + 1;  // over-capacity / empty sequences make reset() fail the env
+      rec->time_limit = time_limit;
+    }
+    W::gsync();  // lane 0's global stores before every lane reads the record back
+    reset(rec_base);
+  }
+
   // ---------------------------------------------------------------- reset (:127-186, :260-273)
   // Runs with the hot block in HBM (hot == ghot).
   __device__ __forceinline__ void reset(const uint8_t* rec_base) {
@@ -1456,9 +1515,20 @@ struct Sim {
     const int32_t* tpl = reinterpret_cast<const int32_t*>(rec_base + kResetHeadBytes + 8 * (int64_t)JC);
     const int nj = rec->num_jobs;
     if (nj <= 0) return;
-    const int prev_episode = H<EnvHeader>(O.hdr)->episode;
+    const EnvHeader* prev = H<EnvHeader>(O.hdr);
+    const int prev_episode = W::uni(prev->episode);
+    const int64_t a_nodes = W::uni(prev->acc_nodes), a_edges = W::uni(prev->acc_edges),
+                  a_jobs = W::uni(prev->acc_jobs), a_events = W::uni(prev->acc_events),
+                  a_dec = W::uni(prev->acc_decisions),
+                  a_eps = W::uni(prev->acc_episodes) + (W::uni(prev->num_jobs) > 0 ? 1 : 0);
     h = EnvHeader();
     h.episode = prev_episode + 1;
+    h.acc_nodes = a_nodes;
+    h.acc_edges = a_edges;
+    h.acc_jobs = a_jobs;
+    h.acc_events = a_events;
+    h.acc_decisions = a_dec;
+    h.acc_episodes = a_eps;
     h.time_limit = rec->time_limit;
     rng.s_hi = rec->rng_state_hi;
     rng.s_lo = rec->rng_state_lo;

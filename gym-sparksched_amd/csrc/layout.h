@@ -46,8 +46,9 @@ struct EnvHeader {
   int32_t step_events;
   int32_t src_idx;        // obs source_job_idx at the last observation
   int32_t pad[2];
-  // running sums over observations (SURVEY.md §8d algorithmic-byte accounting)
-  int64_t acc_nodes, acc_edges, acc_jobs, acc_events;
+  // running sums over observations (SURVEY.md §8d algorithmic-byte accounting), kept across resets;
+  // decisions and finished episodes as well (the per-episode counters above restart at reset)
+  int64_t acc_nodes, acc_edges, acc_jobs, acc_events, acc_decisions, acc_episodes;
 };
 static_assert(sizeof(EnvHeader) % 16 == 0, "header must keep 16-B alignment");
 
@@ -98,6 +99,7 @@ struct PoolRec {
 static_assert(sizeof(PoolRec) == 16, "pool record");
 
 constexpr int kNumLevels = 8;  // EXEC_LEVELS (tpch.py:238)
+constexpr int kNumAcc = 8;     // int64 accumulators per env in the obs arena (ob_acc)
 constexpr int kTraceBytes = 32;
 constexpr int64_t kResetHeadBytes = 64;  // ssim_reset_record padded
 static_assert(sizeof(ssim_reset_record) <= kResetHeadBytes, "reset record");
@@ -239,7 +241,7 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
   L->ob_counts = otake(B * SSIM_NUM_COUNTS * 4);
   L->ob_reward = otake(B * 8);
   L->ob_wall_time = otake(B * 8);
-  L->ob_acc = otake(B * 4 * 8);
+  L->ob_acc = otake(B * kNumAcc * 8);
   L->ob_trace = otake(B * (int64_t)cfg.trace_cap * kTraceBytes);
   L->obs_bytes = align16(b);
 

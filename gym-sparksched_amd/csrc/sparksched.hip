@@ -37,6 +37,20 @@ __global__ __launch_bounds__(64) void k_reset(const Params* __restrict__ P, uint
   s.reset(reset + (int64_t)eid * P->L.reset_stride);
 }
 
+// Device-sampled reset of the envs with mode != SSIM_RESET_SKIP (hot block in HBM, like k_reset).
+__global__ __launch_bounds__(64) void k_reset_sampled(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+                                                      uint8_t* reset, const uint8_t* __restrict__ mode,
+                                                      const uint64_t* __restrict__ seeds,
+                                                      const double* __restrict__ limits) {
+  const int eid = blockIdx.x;
+  const int m = mode[eid];
+  if (m == SSIM_RESET_SKIP) return;
+  Sim<WaveHip> s(P, state, g_smem, obs, eid, false);
+  s.load_header();
+  s.reset_sampled(m, seeds != nullptr ? seeds[eid] : 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
+                  reset + (int64_t)eid * P->L.reset_stride);
+}
+
 // kRes: hot block LDS-resident. A compile-time flag (not a runtime select between an LDS and an HBM pointer)
 // so every hot-block access compiles to ds_read/ds_write rather than FLAT instructions.
 template <bool kRes, int kN, int kJ>
@@ -68,11 +82,13 @@ __global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, con
 
 template <bool kRes, int kN, int kJ>
 __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
-                                                int kind, uint64_t seed, int num_steps, int32_t* action_log,
-                                                uint64_t* prof_out) {
+                                                int kind, uint64_t seed, int num_steps, int flags,
+                                                const double* __restrict__ limits, uint8_t* reset,
+                                                int32_t* action_log, uint64_t* prof_out) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
-  if (env_idle(P, state, eid) && action_log == nullptr) return;
+  const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
+  if (env_idle(P, state, eid) && action_log == nullptr && !autoreset) return;
   Sim<WaveHip, kN, kJ> s(P, state, g_smem, obs, eid, kRes);
   s.load_hot();
   for (int k = 0; k < num_steps; ++k) {
@@ -90,6 +106,10 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
     }
     WaveHip::sync();
     s.step_loaded(a);
+    // episode over (terminated, or truncated by the time limit): reset(seed=None) in place
+    if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit))
+      s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
+                      reset + (int64_t)eid * P->L.reset_stride);
   }
   s.save_hot();
 #ifdef SSIM_PROFILE
@@ -125,7 +145,8 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
 // Kernel variant for a layout: LDS-resident instantiations, specialised on (executors, jobs) for the
 // benchmark shape (BASELINE configs[1]: 10 executors, 50 jobs), else the generic ones.
 using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
-using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int32_t*, uint64_t*);
+using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int, const double*, uint8_t*,
+                          int32_t*, uint64_t*);
 static StepFn pick_step(const Params& p) {
   if (!p.O.lds_resident) return k_step<false, 0, 0>;
   if (p.L.num_executors == 10 && p.L.job_cap == 50) return k_step<true, 10, 50>;
@@ -238,15 +259,35 @@ extern "C" int ssim_policy(ssim_handle* h, int32_t kind, uint64_t seed, uint64_t
   return hip_check(hipGetLastError(), "k_policy launch");
 }
 
-extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t* action_log,
-                            void* stream) {
+extern "C" int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
+                               const double* time_limits, int32_t* action_log, void* stream) {
   if (h == nullptr || num_steps < 0) return set_err(SSIM_E_ARG, "ssim_rollout: bad argument");
   if (kind != SSIM_POLICY_FAIR && kind != SSIM_POLICY_FIFO && kind != SSIM_POLICY_RANDOM)
     return set_err(SSIM_E_ARG, "ssim_rollout: unknown policy %d", kind);
+  if ((flags & ~SSIM_ROLLOUT_AUTORESET) != 0) return set_err(SSIM_E_ARG, "ssim_rollout_ex: unknown flags 0x%x", flags);
+  if ((flags & SSIM_ROLLOUT_AUTORESET) && !(h->params.C.job_arrival_gap > 0.0))
+    return set_err(SSIM_E_ARG, "ssim_rollout_ex: auto-reset needs job_arrival_gap in the config");
   const ssim_layout& L = h->params.L;
   hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
-                     dparams(h), h->state, h->obs, kind, seed, num_steps, action_log, (uint64_t*)nullptr);
+                     dparams(h), h->state, h->obs, kind, seed, num_steps, flags, time_limits, h->reset, action_log,
+                     (uint64_t*)nullptr);
   return hip_check(hipGetLastError(), "k_rollout launch");
+}
+
+extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t* action_log,
+                            void* stream) {
+  return ssim_rollout_ex(h, kind, seed, num_steps, 0, nullptr, action_log, stream);
+}
+
+extern "C" int ssim_reset_sampled(ssim_handle* h, const uint8_t* mode, const uint64_t* seeds, const double* time_limits,
+                                  void* stream) {
+  if (h == nullptr || mode == nullptr) return set_err(SSIM_E_ARG, "ssim_reset_sampled: null argument");
+  if (!(h->params.C.job_arrival_gap > 0.0))
+    return set_err(SSIM_E_ARG, "ssim_reset_sampled: the config has no job_arrival_gap");
+  const ssim_layout& L = h->params.L;
+  hipLaunchKernelGGL(k_reset_sampled, dim3(L.num_envs), dim3(64), (size_t)L.scratch_bytes, (hipStream_t)stream,
+                     dparams(h), h->state, h->obs, h->reset, mode, seeds, time_limits);
+  return hip_check(hipGetLastError(), "k_reset_sampled launch");
 }
 
 #ifdef SSIM_PROFILE
@@ -255,7 +296,8 @@ extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed
                                      uint64_t* prof_out, void* stream) {
   const ssim_layout& L = h->params.L;
   hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
-                     dparams(h), h->state, h->obs, kind, seed, num_steps, (int32_t*)nullptr, prof_out);
+                     dparams(h), h->state, h->obs, kind, seed, num_steps, 0, (const double*)nullptr, h->reset,
+                     (int32_t*)nullptr, prof_out);
   return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
 }
 #endif

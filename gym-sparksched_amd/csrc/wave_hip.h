@@ -41,6 +41,10 @@ struct WaveHip {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
+  __device__ static __forceinline__ void gsync() {  // global-memory ordering across the wave's lanes
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
   __device__ static __forceinline__ uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
   __device__ static __forceinline__ int excl_scan(int x, int* total) {
     int v = x;

@@ -4,6 +4,10 @@ from __future__ import annotations
 
 import ctypes as ct
 
+SSIM_RESET_SKIP, SSIM_RESET_CONTINUE, SSIM_RESET_SEED = 0, 1, 2
+NUM_ACC = 8  # int64 accumulators per env (ob_acc): S_act, E_act, J_act, events, decisions, episodes, 0, 0
+ACC_NODES, ACC_EDGES, ACC_JOBS, ACC_EVENTS, ACC_DECISIONS, ACC_EPISODES = range(6)
+SSIM_ROLLOUT_AUTORESET = 0x1
 SSIM_ERR_SPACE = 0x1
 SSIM_ERR_KEY = 0x2
 SSIM_ERR_TOO_MANY = 0x4
@@ -37,6 +41,9 @@ class SsimConfig(ct.Structure):
         ("moving_delay", ct.c_double),
         ("warmup_delay", ct.c_double),
         ("beta", ct.c_double),
+        ("job_arrival_gap", ct.c_double),
+        ("job_arrival_cap", ct.c_int32),
+        ("pad0", ct.c_int32),
     ]
 
 

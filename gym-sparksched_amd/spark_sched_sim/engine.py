@@ -37,6 +37,8 @@ def make_config(env_cfg: dict, num_envs: int, packed: PackedDataset, job_cap: in
         moving_delay=float(env_cfg["moving_delay"]),
         warmup_delay=float(env_cfg["warmup_delay"]),
         beta=float(env_cfg.get("beta", 0.0)),
+        job_arrival_gap=(1 / env_cfg["job_arrival_rate"]) if env_cfg.get("job_arrival_rate") else 0.0,
+        job_arrival_cap=int(env_cfg.get("job_arrival_cap") or 0),
     )
 
 
@@ -63,7 +65,7 @@ def arena_views(arena, L: SsimLayout) -> dict:
         "counts": sl(L.ob_counts, B * _abi.NUM_COUNTS * 4, i32, (B, _abi.NUM_COUNTS)),
         "reward": sl(L.ob_reward, B * 8, f64, (B,)),
         "wall_time": sl(L.ob_wall_time, B * 8, f64, (B,)),
-        "acc": sl(L.ob_acc, B * 32, i64, (B, 4)),
+        "acc": sl(L.ob_acc, B * 8 * _abi.NUM_ACC, i64, (B, _abi.NUM_ACC)),
     }
     if T > 0:
         v["trace"] = arena[L.ob_trace: L.ob_trace + B * T * _abi.TRACE_BYTES].reshape(B, T, _abi.TRACE_BYTES)
@@ -250,10 +252,35 @@ class DeviceEngine:
                                                           a[1].data_ptr(), self._stream()), "ssim_policy")
         return a[0], a[1]
 
-    def rollout(self, kind: int, seed: int, num_steps: int, action_log=None):
+    def reset_sampled(self, mode, seeds=None, time_limits=None):
+        """Device-side reset (ssim_reset_sampled): job sequences sampled by the kernel from each env's
+        Generator stream. mode: uint8 [B] of _abi.SSIM_RESET_* (or one value for all envs); seeds: uint64 [B]
+        for SSIM_RESET_SEED envs; time_limits: float64 [B] (None = +inf)."""
+        t, B = self.torch, self.num_envs
+        m = t.as_tensor(np.broadcast_to(np.asarray(mode, dtype=np.uint8), (B,)).copy(), device=self.device)
+        sd = None
+        if seeds is not None:
+            sd = t.as_tensor(np.asarray(seeds, dtype=np.uint64).view(np.int64).reshape(B), device=self.device)
+        tl = None
+        if time_limits is not None:
+            tl = t.as_tensor(np.asarray(time_limits, dtype=np.float64).reshape(B), device=self.device)
+        self._keep = (m, sd, tl)
+        self._native.check(self._native.lib().ssim_reset_sampled(
+            self.handle, m.data_ptr(), None if sd is None else sd.data_ptr(), None if tl is None else tl.data_ptr(),
+            self._stream()), "ssim_reset_sampled")
+
+    def rollout(self, kind: int, seed: int, num_steps: int, action_log=None, flags: int = 0, time_limits=None):
+        """`num_steps` fused policy+step launches' worth of decisions in ONE kernel launch. flags:
+        _abi.SSIM_ROLLOUT_AUTORESET resets finished episodes in place (limits from `time_limits`)."""
         ptr = action_log.data_ptr() if action_log is not None else None
-        self._native.check(self._native.lib().ssim_rollout(self.handle, kind, seed, num_steps, ptr, self._stream()),
-                           "ssim_rollout")
+        tl = None
+        if time_limits is not None:
+            tl = self.torch.as_tensor(np.asarray(time_limits, dtype=np.float64).reshape(self.num_envs),
+                                      device=self.device) if not hasattr(time_limits, "data_ptr") else time_limits
+        self._keep_tl = tl
+        self._native.check(self._native.lib().ssim_rollout_ex(
+            self.handle, kind, seed, num_steps, flags, None if tl is None else tl.data_ptr(), ptr, self._stream()),
+            "ssim_rollout")
 
     def host_views(self) -> dict:
         return arena_views(self.obs.cpu().numpy(), self.layout)

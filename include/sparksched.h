@@ -52,6 +52,10 @@ typedef struct ssim_config {
   double moving_delay;    /* ms, spark_sched_sim.py:40 */
   double warmup_delay;    /* ms, tpch.py:44 */
   double beta;            /* reward discount, spark_sched_sim.py:44 */
+  /* device-side job-sequence sampling (ssim_reset_sampled, rollout auto-reset; tpch.py:54-73) */
+  double job_arrival_gap; /* 1 / job_arrival_rate, ms (computed by the caller, as Python does) */
+  int32_t job_arrival_cap;/* 0 = no cap (time-limited episodes) */
+  int32_t pad0;
 } ssim_config;
 
 /* Packed TPC-H-format dataset (device pointers). Built on the host from the raw per-query dicts by the
@@ -104,7 +108,8 @@ typedef struct ssim_layout {
   int64_t ob_counts;       /* int32    [16]            see SSIM_OC_* */
   int64_t ob_reward;       /* float64  [1] */
   int64_t ob_wall_time;    /* float64  [1] */
-  int64_t ob_acc;          /* int64    [4]             running sums of S_act, E_act, J_act, events popped */
+  int64_t ob_acc;          /* int64    [8]             running sums over all episodes: S_act, E_act, J_act,
+                                                      events popped, decisions, finished episodes, 0, 0 */
   int64_t ob_trace;       /* float64/int32 trace records, [trace_cap] x 32 B */
 } ssim_layout;
 
@@ -151,11 +156,36 @@ int ssim_step(ssim_handle* h, const int32_t* stage_idx, const int32_t* num_exec,
 int ssim_policy(ssim_handle* h, int32_t kind, uint64_t seed, uint64_t counter, int32_t* stage_idx,
                 int32_t* num_exec, void* stream);
 
+/* Device-side reset: for every env with mode[env] != SSIM_RESET_SKIP the job sequence
+ * is sampled on the device from the env's numpy Generator(PCG64) stream exactly as TPCHDataSampler.
+ * job_sequence does (tpch.py:54-73: integers(22), choice(7 sizes), exponential(1/rate) by numpy's ziggurat),
+ * then the env is reset as by ssim_reset (spark_sched_sim.py:127-186). Device arrays [num_envs]:
+ *   mode        uint8   SSIM_RESET_SKIP | SSIM_RESET_CONTINUE (reset(seed=None): continue the env's stream)
+ *                       | SSIM_RESET_SEED (reset(seed=s): Generator(PCG64(SeedSequence(seeds[env]))))
+ *   seeds       uint64  (may be NULL when no env uses SSIM_RESET_SEED)
+ *   time_limits float64 StochasticTimeLimit limits (+inf = none); NULL = +inf for every env.
+ * Needs job_arrival_gap (and job_arrival_cap or finite limits) in the config. Uses the reset arena as
+ * scratch for the sampled records. */
+#define SSIM_RESET_SKIP 0
+#define SSIM_RESET_CONTINUE 1
+#define SSIM_RESET_SEED 2
+int ssim_reset_sampled(ssim_handle* h, const uint8_t* mode, const uint64_t* seeds, const double* time_limits,
+                       void* stream);
+
 /* Fused rollout: `num_steps` x (device policy -> step) in ONE launch, obs written every step. The random
  * policy's counter is (episode << 32) + decisions of each env. `action_log` (optional, device int32
  * [num_steps][num_envs][2]) receives every action taken, for replay/parity. */
 int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t* action_log,
                  void* stream);
+
+/* ssim_rollout with flags. SSIM_ROLLOUT_AUTORESET: an env whose episode ends (terminated, or truncated by
+ * its time limit: wall_time >= limit) is reset in place on the device with reset(seed=None) semantics
+ * (continuing its RNG stream, as ssim_reset_sampled SSIM_RESET_CONTINUE) and keeps stepping; the new
+ * episode's limit is time_limits[env] (device float64 [num_envs], NULL = +inf). Each env's obs counts
+ * carry its episode number (SSIM_OC_EPISODE). */
+#define SSIM_ROLLOUT_AUTORESET 0x1
+int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
+                    const double* time_limits, int32_t* action_log, void* stream);
 
 /* Per-job results for metrics (spark_sched_sim/metrics.py): t_arrival/t_completed float64 [num_envs][job_cap]
  * and job state int32 [num_envs][job_cap] (0 not arrived, 1 active, 2 completed), any may be NULL. */

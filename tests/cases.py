@@ -176,6 +176,85 @@ def case_reset_continuation(make, dataset, env_cfg, B=3):
             assert float(v["wall_time"][i]) == float(info["wall_time"])
 
 
+SAMPLED_RESET_CONFIGS = [
+    (dict(), 16, 4100, None),
+    (dict(num_executors=50, job_arrival_cap=200), 4, 4200, 3.0e6),
+    (dict(num_executors=3, job_arrival_cap=20, job_arrival_rate=1e-4, moving_delay=500.0, warmup_delay=100.0),
+     16, 4300, 8.0e5),
+]
+
+
+def _time_limits(mean, B, seed):
+    from spark_sched_sim.wrappers import StochasticTimeLimitSampler
+
+    if mean is None:
+        return None
+    smp = StochasticTimeLimitSampler(mean, B, seed=seed)
+    return np.array([smp.sample(i, seed + i) for i in range(B)])
+
+
+def case_sampled_reset(make, dataset, env_cfg, cfg_over, B, seed0, mean_limit):
+    """ssim_reset_sampled: job sequences drawn on the device (SeedSequence seeding, integers/choice, ziggurat
+    exponential: tpch.py:54-73) give exactly the host-sampled reset (numpy), for reset(seed) and, after a
+    stretch of stepping, for reset(seed=None) continuing each env's stream."""
+    cfg = dict(env_cfg, **cfg_over)
+    host, dev = make(cfg, B, dataset, 0), make(cfg, B, dataset, 0)
+    seeds = [seed0 + 37 * i for i in range(B)]
+    lim = _time_limits(mean_limit, B, seed0)
+    opts = None if lim is None else [{"time_limit": float(x)} for x in lim]
+    host.reset(seeds=seeds, options=opts)
+    dev.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=lim)
+    assert np.array_equal(host.snapshot_obs(), dev.snapshot_obs()), "reset(seed) obs"
+    for k in range(60):  # same actions on both
+        si, ne = host.policy(_abi.SSIM_POLICY_FAIR)
+        si, ne = np.array(host.to_numpy(si)), np.array(host.to_numpy(ne))
+        host.step(si, ne)
+        dev.step(si, ne)
+    lim2 = _time_limits(mean_limit, B, seed0 + 1)
+    opts2 = None if lim2 is None else [{"time_limit": float(x)} for x in lim2]
+    host.reset(seeds=None, options=opts2)
+    dev.reset_sampled(_abi.SSIM_RESET_CONTINUE, time_limits=lim2)
+    a, b = host.snapshot_obs(), dev.snapshot_obs()
+    assert np.array_equal(a, b), "reset(seed=None) obs"
+    v = dev.host_views()
+    assert all(int(v["counts"][i][_abi.OC_EPISODE]) == 2 for i in range(B))
+    assert all(int(v["counts"][i][_abi.OC_ERR]) == 0 for i in range(B))
+
+
+def case_autoreset_replay(make, dataset, env_cfg, B=32, K=1500, mean_limit=None, stride=1):
+    """Fused rollout with SSIM_ROLLOUT_AUTORESET: finished episodes (terminated, or truncated by the time
+    limit) restart in place with reset(seed=None). Replaying the logged actions on the oracle, resetting it the
+    same way, reproduces every env's final observation, wall time and episode count."""
+    cfg = dict(env_cfg, num_executors=4, job_arrival_cap=6, job_arrival_rate=1e-4)
+    eng = make(cfg, B, dataset, 0)
+    seeds = [7100 + i for i in range(B)]
+    lim = _time_limits(mean_limit, B, 99) if mean_limit else None
+    opts = None if lim is None else [{"time_limit": float(x)} for x in lim]
+    eng.reset(seeds=seeds, options=opts)
+    log = eng.alloc_action_log(K)
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 5, K, log, flags=_abi.SSIM_ROLLOUT_AUTORESET, time_limits=lim)
+    log = np.asarray(eng.to_numpy(log))
+    v = eng.host_views()
+    episodes = 0
+    for i in range(0, B, stride):
+        limit = float("inf") if lim is None else float(lim[i])
+        o = SparkSchedOracle(cfg, dataset)
+        ob, _ = o.reset(seed=seeds[i], options={"time_limit": limit})
+        ep = 1
+        for k in range(K):
+            ob, rew, term, _, info = o.step({"stage_idx": int(log[k, i, 0]), "num_exec": int(log[k, i, 1])})
+            if term or info["wall_time"] >= limit:
+                ob, _ = o.reset(seed=None, options={"time_limit": limit})
+                ep += 1
+        c = v["counts"][i]
+        assert int(c[_abi.OC_ERR]) == 0, f"env{i}"
+        assert int(c[_abi.OC_EPISODE]) == ep, f"env{i} episodes {int(c[_abi.OC_EPISODE])} != {ep}"
+        assert float(v["wall_time"][i]) == float(o.wall_time)
+        parity.compare_obs(ob, obs_dict(v, i), f"env{i} final")
+        episodes += ep
+    assert episodes > 3 * B // stride, episodes
+
+
 DECIMA_CONFIGS = [
     (dict(), 4, 101, "random", 1),
     (dict(num_executors=50, job_arrival_cap=200, beta=5e-3), 2, 211, "random", 5),

@@ -21,7 +21,7 @@ from spark_sched_sim.engine import _ResetSampler, arena_views, make_config  # no
 
 SO_PATH = os.path.join(HERE, "_hostsim.so")
 SOURCES = [os.path.join(HERE, "hostsim.cpp")] + [
-    os.path.join(REPO, "gym-sparksched_amd", "csrc", f) for f in ("engine.h", "policy.h", "pyset.h", "pcg64.h", "decima.h",
+    os.path.join(REPO, "gym-sparksched_amd", "csrc", f) for f in ("engine.h", "policy.h", "pyset.h", "pcg64.h", "decima.h", "fdlibm.h", "ziggurat.h",
                                                                   "layout.h")] + [
     os.path.join(REPO, "include", "sparksched.h")]
 
@@ -31,7 +31,7 @@ _lib = None
 def build(force: bool = False, extra_flags=()) -> str:
     newest = max(os.path.getmtime(p) for p in SOURCES)
     if force or not os.path.exists(SO_PATH) or os.path.getmtime(SO_PATH) < newest:
-        cmd = ["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function",
+        cmd = ["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
                f"-I{os.path.join(REPO, 'include')}", f"-I{os.path.join(REPO, 'gym-sparksched_amd', 'csrc')}",
                SOURCES[0], "-o", SO_PATH + ".tmp", *extra_flags]
         subprocess.run(cmd, check=True)
@@ -58,6 +58,11 @@ def lib():
         L.hs_job_times.argtypes = [vp, vp, vp, vp]
         L.hs_pyset_trace.argtypes = [vp, ct.c_int, ct.c_int, vp]
         L.hs_decima.argtypes = [vp, ct.c_float, ct.c_float, vp, vp, vp, vp]
+        L.hs_reset_sampled.argtypes = [vp, vp, vp, vp]
+        L.hs_rollout_ex.argtypes = [vp, ct.c_int, ct.c_uint64, ct.c_int, ct.c_int, vp, vp]
+        L.hs_seed_words.argtypes = [ct.c_uint64, vp]
+        L.hs_std_exponential.argtypes = [vp, ct.c_int, vp]
+        L.hs_log1p.argtypes = [vp, ct.c_int, vp]
         _lib = L
     return _lib
 
@@ -116,9 +121,21 @@ class HostEngine:
         lib().hs_policy(self.handle, kind, seed, counter, a[0].ctypes.data, a[1].ctypes.data)
         return a[0].copy(), a[1].copy()
 
-    def rollout(self, kind, seed, num_steps, action_log=None):
+    def reset_sampled(self, mode, seeds=None, time_limits=None):
+        """Device-style reset (job sequences sampled by the engine): mode uint8 [B], seeds uint64 [B]."""
+        m = np.ascontiguousarray(np.broadcast_to(np.asarray(mode, dtype=np.uint8), (self.num_envs,)))
+        sd = None if seeds is None else np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64))
+        tl = None if time_limits is None else np.ascontiguousarray(np.asarray(time_limits, dtype=np.float64))
+        self._keep = (m, sd, tl)
+        lib().hs_reset_sampled(self.handle, m.ctypes.data, None if sd is None else sd.ctypes.data,
+                               None if tl is None else tl.ctypes.data)
+
+    def rollout(self, kind, seed, num_steps, action_log=None, flags=0, time_limits=None):
         ptr = action_log.ctypes.data if action_log is not None else None
-        rc = lib().hs_rollout(self.handle, kind, seed, num_steps, ptr)
+        tl = None if time_limits is None else np.ascontiguousarray(np.asarray(time_limits, dtype=np.float64))
+        self._keep_tl = tl
+        rc = lib().hs_rollout_ex(self.handle, kind, seed, num_steps, flags, None if tl is None else tl.ctypes.data,
+                                 ptr)
         assert rc == 0, "hostsim rollout: the hot-block policy view disagreed with the obs-arena view" if rc == -5 \
             else f"hostsim rollout rc={rc}"
 

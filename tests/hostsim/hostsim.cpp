@@ -7,6 +7,7 @@
 #define __device__
 #define __host__
 #define __forceinline__ inline
+#define __constant__
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -36,6 +37,7 @@ struct WaveSerial {
   static int writelane(int v, int, int) { return v; }
   static int compact(uint64_t, int v) { return v; }
   static void sync() {}
+  static void gsync() {}
   static uint64_t clock() { return 0; }
   static int excl_scan(int x, int* total) {
     *total = x;
@@ -132,7 +134,26 @@ int hs_policy(hs_handle* h, int kind, uint64_t seed, uint64_t counter, int32_t* 
   return 0;
 }
 
+int hs_reset_sampled(hs_handle* h, const uint8_t* mode, const uint64_t* seeds, const double* limits) {
+  const Params* P = h->params;
+  for (int e = 0; e < P->L.num_envs; ++e) {
+    if (mode[e] == SSIM_RESET_SKIP) continue;
+    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
+    s.load_header();
+    s.reset_sampled(mode[e], seeds ? seeds[e] : 0ull, limits ? limits[e] : __builtin_inf(),
+                    h->reset + (int64_t)e * P->L.reset_stride);
+  }
+  return 0;
+}
+
+int hs_rollout_ex(hs_handle* h, int kind, uint64_t seed, int num_steps, int flags, const double* limits,
+                  int32_t* action_log);
 int hs_rollout(hs_handle* h, int kind, uint64_t seed, int num_steps, int32_t* action_log) {
+  return hs_rollout_ex(h, kind, seed, num_steps, 0, nullptr, action_log);
+}
+
+int hs_rollout_ex(hs_handle* h, int kind, uint64_t seed, int num_steps, int flags, const double* limits,
+                  int32_t* action_log) {
   const Params* P = h->params;
   const int B = P->L.num_envs;
   for (int e = 0; e < B; ++e) {
@@ -149,6 +170,10 @@ int hs_rollout(hs_handle* h, int kind, uint64_t seed, int num_steps, int32_t* ac
         action_log[((int64_t)k * B + e) * 2 + 1] = a.num_exec;
       }
       s.step_loaded(a);
+      if ((flags & SSIM_ROLLOUT_AUTORESET) && s.h.num_jobs > 0 && !s.frozen() &&
+          (s.h.terminated || s.h.wall >= s.h.time_limit))
+        s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits ? limits[e] : __builtin_inf(),
+                        h->reset + (int64_t)e * P->L.reset_stride);
     }
   }
   return 0;
@@ -200,6 +225,32 @@ void hs_pcg_run(uint64_t* words, const int32_t* ops, int n_ops, double* out) {
   words[3] = r.i_lo;
   words[4] = r.has32;
   words[5] = r.u32;
+}
+
+// Seeded PCG64 (SeedSequence) words, then `n` standard exponentials; log1p on given inputs.
+void hs_seed_words(uint64_t seed, uint64_t* words) {
+  const Pcg64 r = Pcg64::from_seed(seed);
+  words[0] = r.s_hi;
+  words[1] = r.s_lo;
+  words[2] = r.i_hi;
+  words[3] = r.i_lo;
+}
+void hs_std_exponential(uint64_t* words, int n, double* out) {
+  Pcg64 r;
+  r.s_hi = words[0];
+  r.s_lo = words[1];
+  r.i_hi = words[2];
+  r.i_lo = words[3];
+  r.has32 = (uint32_t)words[4];
+  r.u32 = (uint32_t)words[5];
+  for (int k = 0; k < n; ++k) out[k] = r.std_exponential();
+  words[0] = r.s_hi;
+  words[1] = r.s_lo;
+  words[4] = r.has32;
+  words[5] = r.u32;
+}
+void hs_log1p(const double* x, int n, double* out) {
+  for (int k = 0; k < n; ++k) out[k] = fd_log1p(x[k]);
 }
 
 // Runs a trace of set operations; after each op writes the iteration order into `orders`

@@ -58,3 +58,13 @@ def test_reset_continuation(make, dataset, env_cfg):
 @pytest.mark.parametrize("cfg_over,B,seed0,pol,every", cases.DECIMA_CONFIGS)
 def test_decima_features(make, dataset, env_cfg, cfg_over, B, seed0, pol, every):
     cases.case_decima_features(make, dataset, env_cfg, cfg_over, B, seed0, pol, every)
+
+
+@pytest.mark.parametrize("cfg_over,B,seed0,mean_limit", cases.SAMPLED_RESET_CONFIGS)
+def test_sampled_reset(make, dataset, env_cfg, cfg_over, B, seed0, mean_limit):
+    cases.case_sampled_reset(make, dataset, env_cfg, cfg_over, B, seed0, mean_limit)
+
+
+@pytest.mark.parametrize("mean_limit", [None, 2.0e5])
+def test_autoreset_replay(make, dataset, env_cfg, mean_limit):
+    cases.case_autoreset_replay(make, dataset, env_cfg, B=48, K=1500, mean_limit=mean_limit, stride=3)

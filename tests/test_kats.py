@@ -126,3 +126,46 @@ def test_pyset_model_matches_cpython(n_keys):
 @pytest.mark.parametrize("n", [1, 3, 5, 7, 10, 16, 50, 64, 99, 100, 150])
 def test_executor_intervals_match_oracle(n):
     assert np.array_equal(executor_intervals(n), R.executor_intervals(n))
+
+
+@pytest.mark.parametrize("seeds", [list(range(64)), [2**32 - 1, 2**32, 2**40 + 7, 2**63 + 5, 98765432101]])
+def test_seedsequence_pcg64_seeding(seeds):
+    """Pcg64::from_seed == Generator(PCG64(SeedSequence(seed))) (gymnasium reset(seed), spark_sched_sim.py:130)."""
+    out = np.zeros(4, dtype=np.uint64)
+    for s in seeds:
+        lib().hs_seed_words(s, out.ctypes.data)
+        st = np.random.PCG64(np.random.SeedSequence(s)).state["state"]
+        m = (1 << 64) - 1
+        assert [int(x) for x in out] == [st["state"] >> 64, st["state"] & m, st["inc"] >> 64, st["inc"] & m], s
+
+
+@pytest.mark.parametrize("seed,pre", [(3, 0), (2024, 1), (77, 3)])
+def test_std_exponential_matches_numpy(seed, pre):
+    """Pcg64::std_exponential (ziggurat tables from csrc/ziggurat.h, tail via fd_log1p) == numpy's
+    Generator.standard_exponential over 300k draws, after `pre` integers() so the buffered uint32 is live."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    for _ in range(pre):
+        rng.integers(22)
+    w = _words(rng)
+    n = 300000
+    got = np.zeros(n)
+    lib().hs_std_exponential(w.ctypes.data, n, got.ctypes.data)
+    ref = rng.standard_exponential(n)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+    assert (int(w[0]) << 64 | int(w[1])) == rng.bit_generator.state["state"]["state"]
+
+
+def test_log1p_matches_libm():
+    """fd_log1p (csrc/fdlibm.h) == the host libm's log1p numpy calls, on the ziggurat tail's inputs
+    x = -u, u a 53-bit uniform, plus small-|x| and branch-boundary inputs."""
+    import math
+
+    rs = np.random.default_rng(5)
+    u = rs.integers(0, 2**53, size=400000, dtype=np.int64).astype(np.float64) * (1.0 / 9007199254740992.0)
+    small = np.ldexp(u[:50000], -rs.integers(1, 60, size=50000))
+    edge = -(float.fromhex("-0x1.2bec4p-2") + np.ldexp(rs.integers(-10**6, 10**6, size=50000).astype(np.float64), -60))
+    x = np.concatenate([-u, -small, -edge, [-0.0, 0.0, -0.5, -1e-300, -(1 - 2**-53)]])
+    got = np.zeros_like(x)
+    lib().hs_log1p(x.ctypes.data, len(x), got.ctypes.data)
+    ref = np.array([math.log1p(v) for v in x])
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
