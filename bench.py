@@ -27,6 +27,21 @@ for _p in (REPO, os.path.join(REPO, "gym-sparksched_amd")):
 
 ENV_CFG = {"num_executors": 10, "job_arrival_cap": 50, "job_arrival_rate": 4.0e-5, "moving_delay": 2000.0,
            "warmup_delay": 1000.0}  # examples.py:15-23
+# BASELINE.json configs: "tpch" = configs[1] (the metric's config, default), "decima" = configs[2] (Decima GNN
+# policy on the GPU vector env, env section of config/decima_tpch.yaml:80-87), "large" = configs[3]'s per-GPU
+# shard (4096 of the 32k envs, 200 jobs / 100 executors, Poisson arrivals, mean_time_limit 2e7 ms).
+WORKLOADS = {
+    "tpch": dict(cfg=ENV_CFG, envs=1024, mean_time_limit=None,
+                 desc="{B} envs/GPU x TPC-H 50 jobs / 10 executors, random valid actions (BASELINE configs[1])"),
+    "decima": dict(cfg={"num_executors": 50, "job_arrival_cap": 200, "job_arrival_rate": 4.0e-5,
+                        "moving_delay": 2000.0, "warmup_delay": 1000.0}, envs=4096, mean_time_limit=2.0e7,
+                   desc="{B} envs/GPU x TPC-H 200-job cap / 50 executors, Decima GNN policy (random init) in "
+                        "PyTorch-ROCm on device obs (BASELINE configs[2])"),
+    "large": dict(cfg={"num_executors": 100, "job_arrival_cap": 200, "job_arrival_rate": 4.0e-5,
+                       "moving_delay": 2000.0, "warmup_delay": 1000.0}, envs=4096, mean_time_limit=2.0e7,
+                  desc="{B} envs/GPU x TPC-H 200-job cap / 100 executors, Poisson arrivals, time limits, random "
+                       "valid actions (BASELINE configs[3] per-GPU shard)"),
+}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -95,7 +110,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="tpch")
+    ap.add_argument("--envs", type=int, default=0, help="envs per GPU (0 = the workload's)")
     ap.add_argument("--mode", choices=["rollout", "step"], default="rollout")
     ap.add_argument("--chunk", type=int, default=0,
                     help="rollout mode: steps per fused launch (0 = --steps). Warmup runs in launches of the same "
@@ -124,14 +140,32 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     dev = torch.device(f"cuda:{local}")
 
-    B, K, W = args.envs, args.steps, args.warmup
-    eng = DeviceEngine(ENV_CFG, B, generate(0), device=dev)
-    eng.reset(seeds=shard_seeds(rank, B, args.seed))
+    wl = WORKLOADS[args.workload]
+    cfg = wl["cfg"]
+    B, K, W = args.envs or wl["envs"], args.steps, args.warmup
+    if args.workload == "decima":
+        args.mode = "decima"
+    eng = DeviceEngine(cfg, B, generate(0), device=dev)
+    seeds = shard_seeds(rank, B, args.seed)
+    limits = None
+    if wl["mean_time_limit"]:  # StochasticTimeLimit (wrappers/stochastic_time_limit.py:5-31), per env
+        from spark_sched_sim.wrappers import StochasticTimeLimitSampler
+
+        smp = StochasticTimeLimitSampler(wl["mean_time_limit"], B, seed=42)
+        limits = torch.tensor([smp.sample(i, int(seeds[i])) for i in range(B)], dtype=torch.float64, device=dev)
+    eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=None if limits is None else limits.cpu().numpy())
     kind = _abi.SSIM_POLICY_RANDOM
     stream = torch.cuda.current_stream(dev)
 
     chunk = args.chunk if args.chunk > 0 else K
     flags = 0 if args.no_autoreset else _abi.SSIM_ROLLOUT_AUTORESET
+    if args.mode == "decima":
+        from spark_sched_sim.schedulers.decima import DecimaScheduler, build_batch
+
+        torch.manual_seed(args.seed)
+        pol = DecimaScheduler(cfg["num_executors"]).to(dev)  # decima_tpch.yaml:66-78 dims, random init
+        gen = torch.Generator(device=dev).manual_seed(args.seed)
+        cnt = eng.views["counts"]
 
     def chunks(n):
         return [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
@@ -141,9 +175,20 @@ def main():
             for k, c in enumerate(chunks(n)):
                 if events is not None:
                     events[2 * k].record(stream)
-                eng.rollout(kind, 1234, c, flags=flags)
+                eng.rollout(kind, 1234, c, flags=flags, time_limits=limits)
                 if events is not None:
                     events[2 * k + 1].record(stream)
+        elif args.mode == "decima":
+            for k in range(n):
+                b = build_batch(eng.views, eng.decima_features())
+                act = pol.schedule(b, generator=gen)
+                if events is not None:
+                    events[2 * k].record(stream)
+                eng.step(act["stage_idx"], act["num_exec"])
+                if events is not None:
+                    events[2 * k + 1].record(stream)
+                done = ((cnt[:, _abi.OC_TERMINATED] != 0) | (cnt[:, _abi.OC_TRUNCATED] != 0)).to(torch.uint8)
+                eng.reset_sampled(done, time_limits=limits)  # finished episodes: reset(seed=None) on device
         else:
             for k in range(n):
                 si, ne = eng.policy(kind, 1234, run.counter)
@@ -211,11 +256,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64+i32",
-            "data": "synthetic TPC-H-format dataset (seeded generator), random valid actions (device RNG)",
-            "config": {"workload": f"{B} envs/GPU x TPC-H 50 jobs / 10 executors (BASELINE configs[1])",
-                       "envs_per_gpu": B, "jobs": 50, "executors": 10, "mode": args.mode,
+            "data": "synthetic TPC-H-format dataset (seeded generator), " + (
+                "Decima GNN policy, random-init weights" if args.mode == "decima" else
+                "random valid actions (device RNG)"),
+            "config": {"workload": wl["desc"].format(B=B), "envs_per_gpu": B,
+                       "jobs": cfg["job_arrival_cap"], "executors": cfg["num_executors"],
+                       "mean_time_limit": wl["mean_time_limit"], "mode": args.mode,
                        "steps_per_launch": chunk if args.mode == "rollout" else 1,
-                       "autoreset": bool(args.mode == "rollout" and flags),
+                       "autoreset": bool(args.mode != "step" and (flags or args.mode == "decima")),
                        "parallelism": f"env-sharded x{world}"},
             "decisions": int(decisions),
             "terminated_envs": int(terminated),
@@ -230,7 +278,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes / world / launches},
             "cpu_baseline": None,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.workload == "tpch":
             procs = args.cpu_procs or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, procs)
         print(json.dumps(line), flush=True)

@@ -257,12 +257,19 @@ class DeviceEngine:
         Generator stream. mode: uint8 [B] of _abi.SSIM_RESET_* (or one value for all envs); seeds: uint64 [B]
         for SSIM_RESET_SEED envs; time_limits: float64 [B] (None = +inf)."""
         t, B = self.torch, self.num_envs
-        m = t.as_tensor(np.broadcast_to(np.asarray(mode, dtype=np.uint8), (B,)).copy(), device=self.device)
+        if isinstance(mode, t.Tensor):  # device tensors are used in place (no host round trip)
+            m = mode.to(device=self.device, dtype=t.uint8).contiguous()
+        else:
+            m = t.as_tensor(np.broadcast_to(np.asarray(mode, dtype=np.uint8), (B,)).copy(), device=self.device)
         sd = None
-        if seeds is not None:
+        if isinstance(seeds, t.Tensor):
+            sd = seeds.to(device=self.device, dtype=t.int64).contiguous()
+        elif seeds is not None:
             sd = t.as_tensor(np.asarray(seeds, dtype=np.uint64).view(np.int64).reshape(B), device=self.device)
         tl = None
-        if time_limits is not None:
+        if isinstance(time_limits, t.Tensor):
+            tl = time_limits.to(device=self.device, dtype=t.float64).contiguous()
+        elif time_limits is not None:
             tl = t.as_tensor(np.asarray(time_limits, dtype=np.float64).reshape(B), device=self.device)
         self._keep = (m, sd, tl)
         self._native.check(self._native.lib().ssim_reset_sampled(

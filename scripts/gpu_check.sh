@@ -18,10 +18,12 @@ step() {
 for s in "$@"; do
   case "$s" in
     smoke)   step smoke 300 python __graft_entry__.py ;;
-    pytest)  step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    pytest)  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench)   step bench 400 python bench.py ;;
     bench_nocpu) step bench_nocpu 300 python bench.py --no-cpu-baseline ;;
     bench_step) step bench_step 300 python bench.py --no-cpu-baseline --mode step ;;
+    bench_decima) step bench_decima 400 python bench.py --workload decima --steps 40 --warmup 5 ;;
+    bench_large) step bench_large 400 python bench.py --workload large --steps 100 --warmup 20 ;;
     prof)    step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     phase)   step phase 600 python scripts/phase_profile.py ;;
     prof_step) step prof_step 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_step" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step --steps 100 ;;

@@ -292,3 +292,118 @@ def case_decima_features(make, dataset, env_cfg, cfg_over, B, seed0, pol, every)
     parity.run_lockstep(eng, oracles, seeds=[seed0 + i for i in range(B)], policy_factory=fac, check_every=50,
                         hook=hook)
     assert seen["checks"] > 50 and seen["masked"] > 10, seen
+
+
+POLICY_CONFIGS = [
+    (dict(), 4, 610, 7),
+    (dict(num_executors=50, job_arrival_cap=200, beta=5e-3), 2, 620, 11),
+]
+
+
+def case_decima_policy(make, dataset, env_cfg, cfg_over, B, seed0, every, device="cpu", max_steps=400):
+    """The batched Decima GNN (spark_sched_sim/schedulers/decima.py) on the engine's device observation and
+    features equals the per-observation CPU fp32 restatement (oracle/decima_gnn.py) on the oracle's
+    reference-format observation: stage scores, exec scores of the first schedulable stage's job, and the
+    evaluate_actions log-probabilities / entropies (collated-batch semantics), within 1e-5."""
+    import torch
+
+    from oracle import decima_gnn as G
+    from spark_sched_sim.schedulers.decima import DecimaScheduler, build_batch
+
+    cfg = dict(env_cfg, **cfg_over)
+    N = cfg["num_executors"]
+    eng = make(cfg, B, dataset, 0)
+    oracles = [SparkSchedOracle(cfg, dataset) for _ in range(B)]
+    torch.manual_seed(seed0)
+    pol = DecimaScheduler(N).to(device)
+    for p in pol.parameters():  # non-zero biases too, so the bias paths are exercised
+        p.data.add_(0.05 * torch.randn_like(p))
+    sd = {k: v.detach().cpu().float() for k, v in pol.state_dict().items()}
+    seen = {"checks": 0, "mp": 0}
+    tol = dict(rtol=1e-5, atol=1e-5)
+
+    def tt(x):
+        return x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x))
+
+    def hook(k, obs, live):
+        if k % every != 0:
+            return
+        feats = {key: tt(x).to(device) for key, x in eng.decima_features_np().items()}
+        v = {key: tt(x).to(device) for key, x in eng.host_views().items() if key != "trace"}
+        alive = torch.tensor(live, device=device)
+        b = build_batch(v, feats, env_mask=alive)
+        with torch.no_grad():
+            h = pol.encoder(b, per_obs_no_mp=True)
+            scores = pol.stage_policy_network(b, h).cpu()
+        base = (torch.cumsum(b.num_stage_acts, 0) - b.num_stage_acts).cpu()
+        stage_sel, job_sel, exec_sel, refs = [], [], [], []
+        for i in range(B):
+            if not live[i]:
+                stage_sel.append(0), job_sel.append(0), exec_sel.append(0)
+                continue
+            ro = decima_observation(obs[i], N)
+            enc = G.encode(sd, ro)
+            rs = G.stage_scores(sd, ro, enc)
+            ns = int(b.num_stage_acts[i])
+            got = scores[int(base[i]): int(base[i]) + ns]
+            assert torch.allclose(got, rs, **tol), f"env{i} step{k}: stage scores\n{got}\n{rs}"
+            si = (k + i) % ns
+            j = G.job_of_stage(ro, si)
+            re = G.exec_scores(sd, ro, enc, j, N)
+            with torch.no_grad():
+                es, _, _ = pol.exec_policy_network(b, h, (b.obs_ptr[i] + j).view(1), torch.tensor([i], device=device))
+            assert torch.allclose(es.cpu(), re, **tol), f"env{i} step{k}: exec scores"
+            ei = (k * 7 + i) % re.numel()
+            stage_sel.append(si), job_sel.append(j), exec_sel.append(ei)
+            refs.append((i, ro, si, j, ei))
+            seen["checks"] += 1
+        if not refs:
+            return
+        # evaluate_actions over the live envs as one collated batch (scheduler.py:103-145)
+        idx = torch.tensor([r[0] for r in refs], device=device)
+        b2 = build_batch({key: x[idx] for key, x in v.items()}, {key: x[idx] for key, x in feats.items()})
+        ev = pol.evaluate_actions(b2, torch.tensor([r[2] for r in refs], device=device),
+                                  torch.tensor([r[3] for r in refs], device=device),
+                                  torch.tensor([r[4] for r in refs], device=device))
+        mp = b2.max_levels > 0
+        seen["mp"] += int(mp)
+        for n, (i, ro, si, j, ei) in enumerate(refs):
+            enc = G.encode(sd, ro, collated_mp=mp)
+            slp, sent = G.evaluate(G.stage_scores(sd, ro, enc), si)
+            elp, eent = G.evaluate(G.exec_scores(sd, ro, enc, j, N), ei)
+            nn_ = ro["nodes"].shape[0]
+            ent = (sent + eent) / float(np.log(np.float32(N * nn_)))
+            assert abs(float(ev["lgprobs"][n].detach()) - (slp + elp)) <= 1e-4 + 1e-5 * abs(slp + elp), f"env{i} lgprob"
+            assert abs(float(ev["entropies"][n].detach()) - ent) <= 1e-4 + 1e-5 * abs(ent), f"env{i} entropy"
+
+    fac = lambda i: RandomPolicy(300 + i)  # noqa: E731
+    parity.run_lockstep(eng, oracles, seeds=[seed0 + i for i in range(B)], policy_factory=fac, check_every=50,
+                        max_steps=max_steps, hook=hook)
+    assert seen["checks"] > 20 and seen["mp"] > 0, seen
+
+
+def case_decima_schedule_runs(make, dataset, env_cfg, B=16, steps=30, device="cpu"):
+    """DecimaScheduler.schedule drives the engine: every sampled action is valid (no error bits) and
+    log-probabilities are finite."""
+    import torch
+
+    from spark_sched_sim.schedulers.decima import DecimaScheduler, build_batch
+
+    N = env_cfg["num_executors"]
+    eng = make(env_cfg, B, dataset, 0)
+    eng.reset(seeds=list(range(B)))
+    torch.manual_seed(0)
+    pol = DecimaScheduler(N).to(device)
+    g = torch.Generator(device=device).manual_seed(1)
+
+    def tt(x):
+        return x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x))
+
+    for _ in range(steps):
+        feats = {key: tt(x).to(device) for key, x in eng.decima_features_np().items()}
+        v = {key: tt(x).to(device) for key, x in eng.host_views().items() if key != "trace"}
+        act = pol.schedule(build_batch(v, feats), generator=g)
+        assert torch.isfinite(act["lgprob"]).all()
+        eng.step(act["stage_idx"].cpu().numpy(), act["num_exec"].cpu().numpy())
+        c = eng.host_views()["counts"]
+        assert int(np.count_nonzero(np.asarray(c)[:, _abi.OC_ERR])) == 0
