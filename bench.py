@@ -37,6 +37,9 @@ WORKLOADS = {
                         "moving_delay": 2000.0, "warmup_delay": 1000.0}, envs=4096, mean_time_limit=2.0e7,
                    desc="{B} envs/GPU x TPC-H 200-job cap / 50 executors, Decima GNN policy (random init) in "
                         "PyTorch-ROCm on device obs (BASELINE configs[2])"),
+    "ppo": dict(cfg=None, envs=16, mean_time_limit=2.0e7,
+                desc="full PPO iteration of config/decima_tpch.yaml per GPU ({B} rollouts = 4 job sequences x 4, "
+                     "Decima GNN, GPU rollouts, data-parallel replicas over RCCL) (BASELINE configs[4])"),
     "large": dict(cfg={"num_executors": 100, "job_arrival_cap": 200, "job_arrival_rate": 4.0e-5,
                        "moving_delay": 2000.0, "warmup_delay": 1000.0}, envs=4096, mean_time_limit=2.0e7,
                   desc="{B} envs/GPU x TPC-H 200-job cap / 100 executors, Poisson arrivals, time limits, random "
@@ -105,6 +108,67 @@ def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisi
     return best[1] * decisions_per_launch, os.path.relpath(best[0], REPO)
 
 
+def run_ppo(args):
+    """BASELINE configs[4]: whole PPO iterations (GPU rollouts to episode end with the Decima GNN, returns,
+    baselines, PPO epochs) of config/decima_tpch.yaml; one replica per GPU, gradients averaged over RCCL.
+    `--steps` = timed iterations, `--warmup` = untimed ones; value = rollout decisions / iteration time."""
+    import torch
+    import torch.distributed as dist
+
+    from spark_sched_sim.distributed import rank_world, reduce_timing
+    from spark_sched_sim.trainers import DECIMA_TPCH, PPO
+
+    rank, world, local = rank_world()
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device(f"cuda:{local}")
+    cfg = {k: dict(v) for k, v in DECIMA_TPCH.items()}
+    if args.ppo_time_limit:
+        cfg["env"]["mean_time_limit"] = args.ppo_time_limit
+    ppo = PPO(cfg["agent"], cfg["env"], cfg["trainer"], device=dev)
+    for _ in range(args.warmup):
+        ppo.train(1, log=None)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    dec = 0
+    phases = {"collect_s": 0.0, "learn_s": 0.0}
+    for _ in range(args.steps):
+        ta = time.perf_counter()
+        buf = ppo.collect()
+        torch.cuda.synchronize(dev)
+        tb = time.perf_counter()
+        ppo.episode_stats()
+        learn = ppo.train_on_rollouts(buf)
+        torch.cuda.synchronize(dev)
+        phases["collect_s"] += tb - ta
+        phases["learn_s"] += time.perf_counter() - tb
+        dec += len(buf)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats = reduce_timing(torch.tensor([elapsed, float(dec)], dtype=torch.float64, device=dev), world)
+    elapsed, dec = stats.tolist()
+    if rank == 0:
+        B = ppo.num_sequences * ppo.num_rollouts
+        print(json.dumps({
+            "metric": "scheduling decisions/sec (env steps/s)", "value": dec / elapsed, "unit": "decisions/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 (GNN) + f64/i32 (sim)",
+            "data": "synthetic TPC-H-format dataset (seeded generator), Decima GNN random init",
+            "config": {"workload": WORKLOADS["ppo"]["desc"].format(B=B), "envs_per_gpu": B,
+                       "mean_time_limit": cfg["env"]["mean_time_limit"], "mode": "ppo",
+                       "parallelism": f"data-parallel x{world}"},
+            "decisions": int(dec), "seconds_per_iteration": elapsed / args.steps,
+            "phase_seconds_rank0": phases, "last_learning_stats": learn,
+            "roofline": None, "cpu_baseline": None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -121,6 +185,8 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--ppo-time-limit", type=float, default=0.0,
+                    help="ppo workload: override mean_time_limit (ms) of config/decima_tpch.yaml (0 = keep 2e7)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="rollout mode: leave finished envs idle instead of resetting them on the device")
     args = ap.parse_args()
@@ -140,6 +206,8 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     dev = torch.device(f"cuda:{local}")
 
+    if args.workload == "ppo":
+        return run_ppo(args)
     wl = WORKLOADS[args.workload]
     cfg = wl["cfg"]
     B, K, W = args.envs or wl["envs"], args.steps, args.warmup

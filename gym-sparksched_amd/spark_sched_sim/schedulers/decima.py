@@ -116,6 +116,69 @@ def build_batch(views: dict, feats: dict, env_mask: torch.Tensor | None = None) 
                     num_stage_acts=num_stage_acts, num_nodes=n, num_envs=B)
 
 
+def select_envs(b: DagBatch, envs: torch.Tensor) -> DagBatch:
+    """Sub-batch of the observations `envs` (i64 indices into b's env rows, any order), renumbered 0..K-1
+    in the given order (the rollout buffer keeps alive envs' observations this way)."""
+    dev = b.x.device
+    envs = envs.to(dev).long()
+    K = envs.numel()
+    n_sel = b.num_nodes[envs]
+    node_base_old = torch.cumsum(b.num_nodes, 0) - b.num_nodes
+    node_start_new = torch.cumsum(n_sel, 0) - n_sel
+    Nt = int(n_sel.sum().item()) if K else 0
+    new_env_of_node = torch.repeat_interleave(torch.arange(K, device=dev), n_sel, output_size=Nt)
+    src_node = node_base_old[envs][new_env_of_node] + (torch.arange(Nt, device=dev) - node_start_new[new_env_of_node])
+    old2new = torch.full((b.x.shape[0],), -1, dtype=torch.long, device=dev)
+    old2new[src_node] = torch.arange(Nt, device=dev)
+    nd_old = b.obs_ptr[1:] - b.obs_ptr[:-1]
+    nd_sel = nd_old[envs]
+    Gt = int(nd_sel.sum().item()) if K else 0
+    new_env_of_dag = torch.repeat_interleave(torch.arange(K, device=dev), nd_sel, output_size=Gt)
+    dag_start_new = torch.cumsum(nd_sel, 0) - nd_sel
+    src_dag = b.obs_ptr[envs][new_env_of_dag] + (torch.arange(Gt, device=dev) - dag_start_new[new_env_of_dag])
+    dag_old2new = torch.full((b.ptr.numel() - 1,), -1, dtype=torch.long, device=dev)
+    dag_old2new[src_dag] = torch.arange(Gt, device=dev)
+    ekeep = old2new[b.edge_index[0]] >= 0
+    ei = old2new[b.edge_index[:, ekeep]]
+    eb = b.edge_bits[ekeep]
+    order = torch.argsort(ei[0] * max(Nt, 1) + ei[1], stable=True) if ei.shape[1] else None
+    if order is not None:  # keep edges grouped per observation in the new env order
+        ei, eb = ei[:, order], eb[order]
+    dag_counts = (b.ptr[1:] - b.ptr[:-1])[src_dag]
+    ptr = torch.zeros(Gt + 1, dtype=torch.long, device=dev)
+    ptr[1:] = torch.cumsum(dag_counts, 0)
+    obs_ptr = torch.zeros(K + 1, dtype=torch.long, device=dev)
+    obs_ptr[1:] = torch.cumsum(nd_sel, 0)
+    lv = b.env_levels[envs]
+    return DagBatch(x=b.x[src_node], edge_index=ei, edge_bits=eb, max_levels=int(lv.max().item()) if K else 0,
+                    env_levels=lv, ptr=ptr, node_dag=dag_old2new[b.node_dag[src_node]], node_env=new_env_of_node,
+                    dag_env=new_env_of_dag, obs_ptr=obs_ptr, stage_mask=b.stage_mask[src_node],
+                    exec_cap=b.exec_cap[src_dag], num_stage_acts=b.num_stage_acts[envs], num_nodes=n_sel,
+                    num_envs=K)
+
+
+def cat_batches(bs: list[DagBatch]) -> DagBatch:
+    """Concatenation of batches (observations in list order)."""
+    dev = bs[0].x.device
+    n_off = torch.tensor([0] + [b.x.shape[0] for b in bs], device=dev).cumsum(0)
+    g_off = torch.tensor([0] + [b.ptr.numel() - 1 for b in bs], device=dev).cumsum(0)
+    e_off = torch.tensor([0] + [b.num_envs for b in bs], device=dev).cumsum(0)
+    lv = torch.cat([b.env_levels for b in bs])
+    return DagBatch(
+        x=torch.cat([b.x for b in bs]),
+        edge_index=torch.cat([b.edge_index + n_off[i] for i, b in enumerate(bs)], dim=1),
+        edge_bits=torch.cat([b.edge_bits for b in bs]),
+        max_levels=max(b.max_levels for b in bs), env_levels=lv,
+        ptr=torch.cat([bs[0].ptr[:1]] + [b.ptr[1:] + n_off[i] for i, b in enumerate(bs)]),
+        node_dag=torch.cat([b.node_dag + g_off[i] for i, b in enumerate(bs)]),
+        node_env=torch.cat([b.node_env + e_off[i] for i, b in enumerate(bs)]),
+        dag_env=torch.cat([b.dag_env + e_off[i] for i, b in enumerate(bs)]),
+        obs_ptr=torch.cat([bs[0].obs_ptr[:1]] + [b.obs_ptr[1:] + g_off[i] for i, b in enumerate(bs)]),
+        stage_mask=torch.cat([b.stage_mask for b in bs]), exec_cap=torch.cat([b.exec_cap for b in bs]),
+        num_stage_acts=torch.cat([b.num_stage_acts for b in bs]), num_nodes=torch.cat([b.num_nodes for b in bs]),
+        num_envs=int(sum(b.num_envs for b in bs)))
+
+
 def segment_sum(src: torch.Tensor, index: torch.Tensor, size: int) -> torch.Tensor:
     out = torch.zeros((size,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
     return out.index_add_(0, index, src)

@@ -1,0 +1,132 @@
+"""GPU rollout collection (trainers/rollout_worker.py:18-46, 135-157: RolloutBuffer, RolloutWorkerSync).
+
+All envs of one GPU step together: every decision is one batched Decima forward (DecimaScheduler.schedule)
+over the envs still running, one ssim_step launch, and the observation, action, log-probability, reward and
+wall time of every live env are appended to a device-resident buffer. An env is done when terminated or
+truncated by its StochasticTimeLimit (wrappers/stochastic_time_limit.py:26-31); from then on it is held with
+an invalid action (the engine leaves its state untouched, SSIM_ERR_SPACE) until the next collection.
+The reference runs one env per process (RolloutWorkerSync); here a "worker" is a row of the batch.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from .. import _abi
+from ..schedulers.decima import DagBatch, build_batch, cat_batches, select_envs
+
+
+class GpuRolloutBuffer:
+    """Per decision step t: the live envs' observations as one DagBatch (select_envs order = `envs[t]`),
+    actions, log-probs, rewards and the wall time before the step. `trajectories()` pads per-env rows."""
+
+    def __init__(self, num_envs: int):
+        self.num_envs = num_envs
+        self.batches: list[DagBatch] = []
+        self.envs: list[torch.Tensor] = []
+        self.stage_idx: list[torch.Tensor] = []
+        self.job_idx: list[torch.Tensor] = []
+        self.exec_idx: list[torch.Tensor] = []
+        self.lgprobs: list[torch.Tensor] = []
+        self.rewards: list[torch.Tensor] = []
+        self.wall_before: list[torch.Tensor] = []
+        self.final_wall: torch.Tensor | None = None
+
+    def add(self, batch, envs, act, reward, wall_before):
+        self.batches.append(batch)
+        self.envs.append(envs)
+        self.stage_idx.append(act["stage_idx"][envs].long())
+        self.job_idx.append(act["job_idx"][envs])
+        self.exec_idx.append(act["exec_idx"][envs])
+        self.lgprobs.append(act["lgprob"][envs])
+        self.rewards.append(reward)
+        self.wall_before.append(wall_before)
+
+    def __len__(self) -> int:
+        return int(sum(e.numel() for e in self.envs))
+
+    def trajectories(self):
+        """Padded per-env rows: times [B, T+1] (wall before each decision, then the final wall time),
+        rewards [B, T], lengths [B], and for each (env, k) its flat sample index into `samples()`."""
+        dev = self.final_wall.device
+        B = self.num_envs
+        env = torch.cat(self.envs)
+        lengths = torch.bincount(env, minlength=B)
+        T = int(lengths.max().item()) if env.numel() else 0
+        # position of each sample in its env row = number of earlier samples of that env
+        order = torch.arange(env.numel(), device=dev)
+        pos = torch.zeros_like(env)
+        # steps are appended in time order, so a stable sort by env keeps each env's decisions in order
+        perm = torch.argsort(env, stable=True)
+        starts = torch.cumsum(lengths, 0) - lengths
+        pos[perm] = order - starts[env[perm]]
+        times = torch.zeros((B, T + 1), dtype=torch.float64, device=dev)
+        rewards = torch.zeros((B, T), dtype=torch.float64, device=dev)
+        times[env, pos] = torch.cat(self.wall_before)
+        rewards[env, pos] = torch.cat(self.rewards)
+        times[torch.arange(B, device=dev), lengths] = self.final_wall
+        sample = torch.full((B, T), -1, dtype=torch.long, device=dev)
+        sample[env, pos] = order
+        return times, rewards, lengths, sample
+
+    def samples(self) -> tuple[DagBatch, dict[str, torch.Tensor]]:
+        """All stored observations as one DagBatch (sample i = observation row i) and the flat actions."""
+        acts = {"stage_idx": torch.cat(self.stage_idx), "job_idx": torch.cat(self.job_idx),
+                "exec_idx": torch.cat(self.exec_idx), "lgprob": torch.cat(self.lgprobs)}
+        return cat_batches(self.batches), acts
+
+
+class RolloutCollector:
+    """Drives a DeviceEngine (or the test-only HostEngine) with a DecimaScheduler until every env is done."""
+
+    def __init__(self, engine, policy, num_tasks_scale: float = 200.0, work_scale: float = 1e5):
+        self.engine = engine
+        self.policy = policy
+        self.scales = (num_tasks_scale, work_scale)
+        self.on_device = isinstance(engine.views["counts"], torch.Tensor)  # DeviceEngine vs test host build
+
+    def _views(self, features: bool = True):
+        eng = self.engine
+        if self.on_device:
+            return eng.views, (eng.decima_features(*self.scales) if features else None)
+        dev = self.policy.device  # host build: numpy views -> tensors on the policy's device
+        v = {k: torch.from_numpy(x).to(dev) for k, x in eng.host_views().items() if k != "trace"}
+        if not features:
+            return v, None
+        f = {k: torch.from_numpy(x).to(dev) for k, x in eng.decima_features_np(*self.scales).items()}
+        return v, f
+
+    @torch.no_grad()
+    def collect(self, seeds, time_limits=None, generator=None, max_steps: int = 10**9) -> GpuRolloutBuffer:
+        eng = self.engine
+        B = eng.num_envs
+        limits = None if time_limits is None else torch.as_tensor(time_limits, dtype=torch.float64)
+        eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds,
+                          time_limits=None if limits is None else limits.cpu().numpy())
+        v, _ = self._views(features=False)
+        dev = v["counts"].device
+        buf = GpuRolloutBuffer(B)
+        alive = torch.ones(B, dtype=torch.bool, device=dev)
+        wall = torch.zeros(B, dtype=torch.float64, device=dev)
+        for _ in range(max_steps):
+            if not bool(alive.any()):
+                break
+            v, f = self._views()
+            b_all = build_batch(v, f, env_mask=alive)
+            act = self.policy.schedule(b_all, generator=generator)
+            envs = torch.nonzero(alive).squeeze(1)
+            batch = select_envs(b_all, envs)
+            si = torch.where(alive, act["stage_idx"], torch.full_like(act["stage_idx"], -2))
+            if self.on_device:
+                eng.step(si, act["num_exec"])
+            else:
+                eng.step(si.cpu().numpy(), act["num_exec"].cpu().numpy())
+            v, _ = self._views(features=False)
+            c = v["counts"]
+            reward = v["reward"][envs].double()
+            buf.add(batch, envs, act, reward, wall[envs])
+            wall = torch.where(alive, v["wall_time"].double(), wall)
+            done = (c[:, _abi.OC_TERMINATED] != 0) | (c[:, _abi.OC_TRUNCATED] != 0)
+            alive = alive & ~done
+        buf.final_wall = wall
+        return buf

@@ -1,0 +1,188 @@
+"""GPU-resident training pieces (spark_sched_sim/trainers): returns and baselines vs the numpy restatement
+of trainers/utils (oracle/trainer_utils.py); DagBatch select/concat; PPO iterations on the test-only host
+build (CPU), on two gloo ranks (data-parallel replicas stay identical), and on the device (`-m gpu`)."""
+
+import multiprocessing as mp
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import trainer_utils as TU
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SMALL_ENV = dict(num_executors=4, job_arrival_cap=5, job_arrival_rate=1e-4, moving_delay=500.0, warmup_delay=100.0)
+TRAIN = dict(seed=42, num_sequences=2, num_rollouts=2, num_epochs=2, num_batches=3, clip_range=0.2, target_kl=0.5,
+             entropy_coeff=0.04, beta_discount=5e-3, opt_cls="Adam", opt_kwargs={"lr": 3e-4}, max_grad_norm=0.5)
+
+
+def _trajs(rs, R, with_dups=True):
+    times, rewards = [], []
+    for _ in range(R):
+        T = int(rs.integers(3, 40))
+        dt = rs.exponential(3000.0, size=T)
+        if with_dups:
+            dt[rs.random(T) < 0.3] = 0.0  # several decisions at one wall time
+        t = np.concatenate([[0.0], np.cumsum(dt)])
+        times.append(t)
+        rewards.append(-rs.exponential(5e4, size=T))
+    return times, rewards
+
+
+def _pad(times, rewards):
+    R = len(rewards)
+    T = max(len(r) for r in rewards)
+    tt = torch.zeros((R, T + 1), dtype=torch.float64)
+    rr = torch.zeros((R, T), dtype=torch.float64)
+    n = torch.tensor([len(r) for r in rewards])
+    for i in range(R):
+        tt[i, : len(times[i])] = torch.from_numpy(times[i])
+        rr[i, : len(rewards[i])] = torch.from_numpy(rewards[i])
+    return tt, rr, n
+
+
+def test_discounted_returns_and_baseline_match_reference():
+    from spark_sched_sim.trainers.returns import Baseline, ReturnsCalculator
+
+    rs = np.random.default_rng(3)
+    S, R = 3, 4
+    times, rewards = _trajs(rs, S * R)
+    tt, rr, n = _pad(times, rewards)
+    got = ReturnsCalculator(beta=5e-3)(tt, rr, n)
+    ref = TU.discounted_returns(times, rewards, 5e-3)
+    for i in range(S * R):
+        assert np.allclose(got[i, : n[i]].numpy(), ref[i], rtol=1e-12, atol=0)
+    base = Baseline(S, R)(tt[:, :-1], got, n)
+    ref_b = TU.baseline_average([t[:-1] for t in times], ref, S, R)
+    for i in range(S * R):
+        assert np.allclose(base[i, : n[i]].numpy(), ref_b[i], rtol=1e-12, atol=1e-9)
+
+
+def test_differential_returns_match_reference():
+    from spark_sched_sim.trainers.returns import ReturnsCalculator
+
+    rs = np.random.default_rng(4)
+    calc, ref = ReturnsCalculator(buff_cap=50), TU.DifferentialReturns(50)
+    for _ in range(3):  # the moving window carries over iterations
+        times, rewards = _trajs(rs, 4)
+        tt, rr, n = _pad(times, rewards)
+        got = calc(tt, rr, n)
+        want = ref(times, rewards)
+        assert abs(calc.avg_num_jobs - ref.avg_num_jobs) <= 1e-12 * abs(ref.avg_num_jobs)
+        for i in range(4):
+            assert np.allclose(got[i, : n[i]].numpy(), want[i], rtol=1e-9, atol=1e-6)
+
+
+def _host_engine(cfg, n, ds):
+    from hostsim.driver import HostEngine
+
+    return HostEngine(cfg, n, ds)
+
+
+def test_select_and_cat_batches_preserve_scores(dataset):
+    from spark_sched_sim import _abi
+    from spark_sched_sim.schedulers.decima import DecimaScheduler, build_batch, cat_batches, select_envs
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0)
+    eng = _host_engine(cfg, 6, dataset)
+    eng.reset(seeds=list(range(6)))
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 3, 25)
+    v = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.host_views().items() if k != "trace"}
+    f = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.decima_features_np().items()}
+    torch.manual_seed(0)
+    pol = DecimaScheduler(10)
+    full = build_batch(v, f)
+    sel = torch.tensor([4, 1, 5])
+    sub = select_envs(full, sel)
+    again = cat_batches([select_envs(full, sel[:1]), select_envs(full, sel[1:])])
+    with torch.no_grad():
+        # schedule-mode scores are per observation (no cross-observation coupling): a selected/concatenated
+        # batch must give each observation exactly the scores it gets alone
+        alone = []
+        for k in range(3):
+            one = select_envs(full, sel[k:k + 1])
+            alone.append(pol.stage_policy_network(one, pol.encoder(one, per_obs_no_mp=True)))
+        for bb in (sub, again):
+            assert bb.num_envs == 3 and int(bb.num_nodes.sum()) == int(full.num_nodes[sel].sum())
+            assert torch.equal(bb.x, torch.cat([full.x[full.node_env == int(e)] for e in sel]))
+            sc = pol.stage_policy_network(bb, pol.encoder(bb, per_obs_no_mp=True))
+            assert torch.allclose(sc, torch.cat(alone), rtol=1e-6, atol=1e-6)
+
+
+def test_ppo_iteration_host(dataset):
+    from spark_sched_sim.trainers import PPO
+
+    agent = {"embed_dim": 16}
+    ppo = PPO(agent, dict(SMALL_ENV, mean_time_limit=4e5), TRAIN, engine_factory=_host_engine, dataset=dataset,
+              device="cpu")
+    before = [p.detach().clone() for p in ppo.scheduler.parameters()]
+    hist = ppo.train(2, log=None)
+    assert len(hist) == 2 and hist[0]["samples"] > 10
+    assert all(np.isfinite(h["policy loss"]) for h in hist)
+    assert any(not torch.equal(a, b) for a, b in zip(before, ppo.scheduler.parameters()))
+    st = ppo.episode_stats()
+    assert st.shape == (4, 4) and (st[:, 3] >= st[:, 2]).all()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ppo_rank(rank, world, port, q):
+    for p in (HERE, REPO, os.path.join(REPO, "gym-sparksched_amd")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    from spark_sched_sim.data_samplers.synthetic_tpch import generate
+    from spark_sched_sim.trainers import PPO
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ppo = PPO({"embed_dim": 16}, dict(SMALL_ENV, mean_time_limit=4e5), TRAIN, engine_factory=_host_engine,
+                  dataset=generate(0), device="cpu")
+        seeds = ppo._seeds()
+        ppo.train(1, log=None)
+        flat = torch.cat([p.detach().reshape(-1) for p in ppo.scheduler.parameters()]).numpy()
+        q.put((rank, flat, seeds, ppo.episode_stats().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ppo_two_rank_gloo_replicas_stay_identical():
+    from hostsim.driver import build
+
+    build()
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ppo_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, flat, seeds, st = q.get(timeout=600)
+        res[r] = (flat, seeds, st)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0][0], res[1][0])  # gradient all-reduce keeps the replicas bit-identical
+    assert res[0][1] != res[1][1] and set(res[0][1]).isdisjoint(res[1][1])  # disjoint job sequences per rank
+    assert np.array_equal(res[0][2], res[1][2]) and res[0][2].shape == (8, 4)  # gathered stats
+
+
+@pytest.mark.gpu
+def test_ppo_iteration_gpu(gpu_device, dataset):
+    from spark_sched_sim.trainers import PPO
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0,
+               mean_time_limit=2e6)
+    ppo = PPO({"embed_dim": 16}, cfg, dict(TRAIN, num_sequences=4, num_rollouts=4), dataset=dataset,
+              device=gpu_device)
+    hist = ppo.train(2, log=None)
+    assert hist[-1]["samples"] > 100 and np.isfinite(hist[-1]["policy loss"])
