@@ -11,6 +11,11 @@ pass instead of B Python-level calls:
     into their parents (the level's edges come from the device edge-mask bit planes, csrc/decima.h);
   * `pyg.utils.softmax(ptr)` / `random.choices` -> segment softmax + per-env categorical sampling on device.
 
+Launch-bound by design (a decision is ~150 small kernels), so the forward avoids data-dependent shapes:
+one host sync per batch for the sizes, no boolean-mask indexing (every level's message pass runs over all
+nodes/edges with 0/1 edge weights, stage scores over all nodes with -inf for non-schedulable ones, exec
+scores on a dense [envs, N] grid with -inf beyond each DAG's commit cap).
+
 Parameter names match the reference module tree, so a reference `state_dict` loads unchanged.
 
 Semantics kept from the reference, including its two message-passing conventions:
@@ -54,9 +59,9 @@ def make_mlp(input_dim: int, hid_dims: list[int], output_dim: int, act_cls: str,
 
 @dataclass
 class DagBatch:
-    """All envs' observations as one flat graph batch (node rows env-major, DAGs contiguous)."""
+    """All envs' observations as one flat graph batch (node rows env-major, DAGs and edges contiguous per env)."""
     x: torch.Tensor            # f32 [Nt, 5] Decima node features
-    edge_index: torch.Tensor   # i64 [2, Et] (parent, child) in flat node ids
+    edge_index: torch.Tensor   # i64 [2, Et] (parent, child) in flat node ids, env-major
     edge_bits: torch.Tensor    # i32 [Et]    bit l = edge in DAG-layer mask l
     max_levels: int            # max over envs of (depth - 1): message-passing levels
     env_levels: torch.Tensor   # i64 [B]     per env (depth - 1, >= 0)
@@ -69,51 +74,57 @@ class DagBatch:
     exec_cap: torch.Tensor     # i64 [Gt]    exec_mask[g, :cap] = True
     num_stage_acts: torch.Tensor  # i64 [B]
     num_nodes: torch.Tensor       # i64 [B]
+    num_edges: torch.Tensor       # i64 [B]
     num_envs: int
+
+
+def _excl(c: torch.Tensor) -> torch.Tensor:
+    return torch.cumsum(c, 0) - c
+
+
+def _ptr(c: torch.Tensor) -> torch.Tensor:
+    out = torch.zeros(c.numel() + 1, dtype=torch.long, device=c.device)
+    out[1:] = torch.cumsum(c, 0)
+    return out
+
+
+def _expand(counts: torch.Tensor, total: int):
+    """(owner row, index within owner) for `total` items laid out by `counts` (no host sync)."""
+    own = torch.repeat_interleave(torch.arange(counts.numel(), device=counts.device), counts, output_size=total)
+    return own, torch.arange(total, device=counts.device) - _excl(counts)[own]
 
 
 def build_batch(views: dict, feats: dict, env_mask: torch.Tensor | None = None) -> DagBatch:
     """Flat batch from the obs-arena views (DeviceEngine.views) and the device Decima features
-    (DeviceEngine.decima_features). `env_mask` (bool [B]) drops envs (e.g. finished ones)."""
+    (DeviceEngine.decima_features). `env_mask` (bool [B]) empties envs (e.g. finished ones)."""
     c = views["counts"]
     dev = c.device
-    B, S = views["nodes"].shape[:2]
-    E = views["edge_links"].shape[1]
-    J = views["exec_supplies"].shape[1]
+    B = views["nodes"].shape[0]
     n = c[:, _abi.OC_NUM_NODES].long()
     ne = c[:, _abi.OC_NUM_EDGES].long()
     nj = c[:, _abi.OC_NUM_JOBS].long()
     if env_mask is not None:
-        keep = env_mask.to(dev)
+        keep = env_mask.to(dev).long()
         n, ne, nj = n * keep, ne * keep, nj * keep
-    node_valid = torch.arange(S, device=dev)[None, :] < n[:, None]
-    edge_valid = torch.arange(E, device=dev)[None, :] < ne[:, None]
-    job_valid = torch.arange(J, device=dev)[None, :] < nj[:, None]
-    x = feats["node_feats"][node_valid]
-    node_base = torch.cumsum(n, 0) - n
-    env_ids = torch.arange(B, device=dev)
-    edge_env = torch.repeat_interleave(env_ids, ne)
-    links = views["edge_links"][edge_valid]
+    levels = torch.clamp(feats["depth"].long() - 1, min=0) * (n > 0)
+    Nt, Et, Gt, L = (int(v) for v in torch.stack([n.sum(), ne.sum(), nj.sum(), levels.max()]).tolist())
+    node_env, nl = _expand(n, Nt)
+    node_base = _excl(n)
+    x = feats["node_feats"][node_env, nl]
+    stage_mask = views["nodes"][node_env, nl, 2] != 0
+    edge_env, el = _expand(ne, Et)
+    links = views["edge_links"][edge_env, el]
     edge_index = (links + node_base[edge_env][:, None]).t().contiguous()
-    edge_bits = feats["edge_mask"][edge_valid]
-    depth = feats["depth"].long()
-    env_levels = torch.clamp(depth - 1, min=0) * (n > 0)
+    edge_bits = feats["edge_mask"][edge_env, el]
+    dag_env, dl = _expand(nj, Gt)
     dag_ptr = views["dag_ptr"].long()
-    dag_counts = (dag_ptr[:, 1:] - dag_ptr[:, :-1])[job_valid]
-    ptr = torch.zeros(dag_counts.numel() + 1, dtype=torch.long, device=dev)
-    ptr[1:] = torch.cumsum(dag_counts, 0)
-    Nt, Gt = x.shape[0], dag_counts.numel()
-    node_dag = torch.repeat_interleave(torch.arange(Gt, device=dev), dag_counts, output_size=Nt)
-    node_env = torch.repeat_interleave(env_ids, n, output_size=Nt)
-    dag_env = torch.repeat_interleave(env_ids, nj, output_size=Gt)
-    obs_ptr = torch.zeros(B + 1, dtype=torch.long, device=dev)
-    obs_ptr[1:] = torch.cumsum(nj, 0)
-    stage_mask = views["nodes"][:, :, 2][node_valid] != 0
+    dag_counts = dag_ptr[dag_env, dl + 1] - dag_ptr[dag_env, dl]
+    node_dag, _ = _expand(dag_counts, Nt)
     num_stage_acts = torch.zeros(B, dtype=torch.long, device=dev).index_add_(0, node_env, stage_mask.long())
-    return DagBatch(x=x, edge_index=edge_index, edge_bits=edge_bits, max_levels=int(env_levels.max().item()) if B else 0,
-                    env_levels=env_levels, ptr=ptr, node_dag=node_dag, node_env=node_env, dag_env=dag_env,
-                    obs_ptr=obs_ptr, stage_mask=stage_mask, exec_cap=feats["commit_cap"][job_valid].long(),
-                    num_stage_acts=num_stage_acts, num_nodes=n, num_envs=B)
+    return DagBatch(x=x, edge_index=edge_index, edge_bits=edge_bits, max_levels=L, env_levels=levels,
+                    ptr=_ptr(dag_counts), node_dag=node_dag, node_env=node_env, dag_env=dag_env, obs_ptr=_ptr(nj),
+                    stage_mask=stage_mask, exec_cap=feats["commit_cap"][dag_env, dl].long(),
+                    num_stage_acts=num_stage_acts, num_nodes=n, num_edges=ne, num_envs=B)
 
 
 def select_envs(b: DagBatch, envs: torch.Tensor) -> DagBatch:
@@ -122,39 +133,28 @@ def select_envs(b: DagBatch, envs: torch.Tensor) -> DagBatch:
     dev = b.x.device
     envs = envs.to(dev).long()
     K = envs.numel()
-    n_sel = b.num_nodes[envs]
-    node_base_old = torch.cumsum(b.num_nodes, 0) - b.num_nodes
-    node_start_new = torch.cumsum(n_sel, 0) - n_sel
-    Nt = int(n_sel.sum().item()) if K else 0
-    new_env_of_node = torch.repeat_interleave(torch.arange(K, device=dev), n_sel, output_size=Nt)
-    src_node = node_base_old[envs][new_env_of_node] + (torch.arange(Nt, device=dev) - node_start_new[new_env_of_node])
-    old2new = torch.full((b.x.shape[0],), -1, dtype=torch.long, device=dev)
-    old2new[src_node] = torch.arange(Nt, device=dev)
-    nd_old = b.obs_ptr[1:] - b.obs_ptr[:-1]
-    nd_sel = nd_old[envs]
-    Gt = int(nd_sel.sum().item()) if K else 0
-    new_env_of_dag = torch.repeat_interleave(torch.arange(K, device=dev), nd_sel, output_size=Gt)
-    dag_start_new = torch.cumsum(nd_sel, 0) - nd_sel
-    src_dag = b.obs_ptr[envs][new_env_of_dag] + (torch.arange(Gt, device=dev) - dag_start_new[new_env_of_dag])
-    dag_old2new = torch.full((b.ptr.numel() - 1,), -1, dtype=torch.long, device=dev)
-    dag_old2new[src_dag] = torch.arange(Gt, device=dev)
-    ekeep = old2new[b.edge_index[0]] >= 0
-    ei = old2new[b.edge_index[:, ekeep]]
-    eb = b.edge_bits[ekeep]
-    order = torch.argsort(ei[0] * max(Nt, 1) + ei[1], stable=True) if ei.shape[1] else None
-    if order is not None:  # keep edges grouped per observation in the new env order
-        ei, eb = ei[:, order], eb[order]
-    dag_counts = (b.ptr[1:] - b.ptr[:-1])[src_dag]
-    ptr = torch.zeros(Gt + 1, dtype=torch.long, device=dev)
-    ptr[1:] = torch.cumsum(dag_counts, 0)
-    obs_ptr = torch.zeros(K + 1, dtype=torch.long, device=dev)
-    obs_ptr[1:] = torch.cumsum(nd_sel, 0)
+    n, ne = b.num_nodes[envs], b.num_edges[envs]
+    nd = (b.obs_ptr[1:] - b.obs_ptr[:-1])[envs]
     lv = b.env_levels[envs]
-    return DagBatch(x=b.x[src_node], edge_index=ei, edge_bits=eb, max_levels=int(lv.max().item()) if K else 0,
-                    env_levels=lv, ptr=ptr, node_dag=dag_old2new[b.node_dag[src_node]], node_env=new_env_of_node,
-                    dag_env=new_env_of_dag, obs_ptr=obs_ptr, stage_mask=b.stage_mask[src_node],
-                    exec_cap=b.exec_cap[src_dag], num_stage_acts=b.num_stage_acts[envs], num_nodes=n_sel,
-                    num_envs=K)
+    if K == 0:
+        Nt = Et = Gt = L = 0
+    else:
+        Nt, Et, Gt, L = (int(v) for v in torch.stack([n.sum(), ne.sum(), nd.sum(), lv.max()]).tolist())
+    node_base_old, edge_base_old = _excl(b.num_nodes), _excl(b.num_edges)
+    node_env, nl = _expand(n, Nt)
+    src_node = node_base_old[envs][node_env] + nl
+    edge_env, el = _expand(ne, Et)
+    src_edge = edge_base_old[envs][edge_env] + el
+    shift = (_excl(n) - node_base_old[envs])[edge_env]
+    dag_env, dl = _expand(nd, Gt)
+    src_dag = b.obs_ptr[envs][dag_env] + dl
+    dag_shift = (_excl(nd) - b.obs_ptr[envs])[node_env]
+    dag_counts = (b.ptr[1:] - b.ptr[:-1])[src_dag]
+    return DagBatch(x=b.x[src_node], edge_index=b.edge_index[:, src_edge] + shift[None, :],
+                    edge_bits=b.edge_bits[src_edge], max_levels=L, env_levels=lv, ptr=_ptr(dag_counts),
+                    node_dag=b.node_dag[src_node] + dag_shift, node_env=node_env, dag_env=dag_env, obs_ptr=_ptr(nd),
+                    stage_mask=b.stage_mask[src_node], exec_cap=b.exec_cap[src_dag],
+                    num_stage_acts=b.num_stage_acts[envs], num_nodes=n, num_edges=ne, num_envs=K)
 
 
 def cat_batches(bs: list[DagBatch]) -> DagBatch:
@@ -163,12 +163,11 @@ def cat_batches(bs: list[DagBatch]) -> DagBatch:
     n_off = torch.tensor([0] + [b.x.shape[0] for b in bs], device=dev).cumsum(0)
     g_off = torch.tensor([0] + [b.ptr.numel() - 1 for b in bs], device=dev).cumsum(0)
     e_off = torch.tensor([0] + [b.num_envs for b in bs], device=dev).cumsum(0)
-    lv = torch.cat([b.env_levels for b in bs])
     return DagBatch(
         x=torch.cat([b.x for b in bs]),
         edge_index=torch.cat([b.edge_index + n_off[i] for i, b in enumerate(bs)], dim=1),
         edge_bits=torch.cat([b.edge_bits for b in bs]),
-        max_levels=max(b.max_levels for b in bs), env_levels=lv,
+        max_levels=max(b.max_levels for b in bs), env_levels=torch.cat([b.env_levels for b in bs]),
         ptr=torch.cat([bs[0].ptr[:1]] + [b.ptr[1:] + n_off[i] for i, b in enumerate(bs)]),
         node_dag=torch.cat([b.node_dag + g_off[i] for i, b in enumerate(bs)]),
         node_env=torch.cat([b.node_env + e_off[i] for i, b in enumerate(bs)]),
@@ -176,7 +175,7 @@ def cat_batches(bs: list[DagBatch]) -> DagBatch:
         obs_ptr=torch.cat([bs[0].obs_ptr[:1]] + [b.obs_ptr[1:] + g_off[i] for i, b in enumerate(bs)]),
         stage_mask=torch.cat([b.stage_mask for b in bs]), exec_cap=torch.cat([b.exec_cap for b in bs]),
         num_stage_acts=torch.cat([b.num_stage_acts for b in bs]), num_nodes=torch.cat([b.num_nodes for b in bs]),
-        num_envs=int(sum(b.num_envs for b in bs)))
+        num_edges=torch.cat([b.num_edges for b in bs]), num_envs=int(sum(b.num_envs for b in bs)))
 
 
 def segment_sum(src: torch.Tensor, index: torch.Tensor, size: int) -> torch.Tensor:
@@ -184,30 +183,45 @@ def segment_sum(src: torch.Tensor, index: torch.Tensor, size: int) -> torch.Tens
     return out.index_add_(0, index, src)
 
 
-def segment_log_softmax(scores: torch.Tensor, seg: torch.Tensor, nseg: int) -> torch.Tensor:
-    """log of pyg.utils.softmax(scores, index=seg) (utils.py:37), without clamping."""
-    mx = torch.full((nseg,), -torch.inf, dtype=scores.dtype, device=scores.device)
-    mx = mx.scatter_reduce(0, seg, scores, reduce="amax", include_self=True)
-    z = scores - mx[seg]
-    lse = torch.log(segment_sum(torch.exp(z), seg, nseg))
-    return z - lse[seg]
+def segment_max(src: torch.Tensor, index: torch.Tensor, size: int) -> torch.Tensor:
+    """Per-segment max of a detached score vector; empty / all -inf segments give 0 (safe shift)."""
+    mx = torch.full((size,), -torch.inf, dtype=src.dtype, device=src.device)
+    mx = mx.scatter_reduce(0, index, src.detach(), reduce="amax", include_self=True)
+    return torch.where(torch.isfinite(mx), mx, torch.zeros_like(mx))
 
 
-def segment_sample(logp: torch.Tensor, seg: torch.Tensor, nseg: int, generator=None) -> torch.Tensor:
-    """One categorical draw per segment (Gumbel-max over log-probabilities); returns flat row indices
-    (-1 for empty segments)."""
+def masked_softmax_stats(scores: torch.Tensor, mask: torch.Tensor, seg: torch.Tensor, nseg: int, clamp: bool):
+    """pyg.utils.softmax over the masked rows of each segment (utils.py:37): probs (0 off-mask) and log-probs
+    (-inf off-mask). `clamp` applies torch.distributions clamp_probs (utils.py:38) as evaluate() does."""
+    mx = segment_max(torch.where(mask, scores, torch.full_like(scores, -torch.inf)), seg, nseg)
+    z = torch.where(mask, scores - mx[seg], torch.zeros_like(scores))
+    ex = torch.where(mask, torch.exp(z), torch.zeros_like(z))
+    probs = ex / (segment_sum(ex, seg, nseg) + 1e-16)[seg]
+    if clamp:
+        eps = torch.finfo(probs.dtype).eps
+        probs = probs.clamp(min=eps, max=1 - eps)
+    logp = torch.where(mask, torch.log(torch.where(mask, probs, torch.ones_like(probs))),
+                       torch.full_like(probs, -torch.inf))
+    return torch.where(mask, probs, torch.zeros_like(probs)), logp
+
+
+def gumbel_pick(logp: torch.Tensor, seg: torch.Tensor, nseg: int, generator=None) -> torch.Tensor:
+    """One categorical draw per segment from log-probabilities (-inf = excluded): Gumbel-max; returns the flat
+    row index per segment (-1 for segments without a candidate)."""
     u = torch.rand(logp.shape, dtype=torch.float64, device=logp.device, generator=generator)
     g = logp.double() - torch.log(-torch.log(u.clamp_min(1e-300)))
     best = torch.full((nseg,), -torch.inf, dtype=torch.float64, device=logp.device)
     best = best.scatter_reduce(0, seg, g, reduce="amax", include_self=True)
-    hit = g == best[seg]
     rows = torch.arange(logp.numel(), device=logp.device)
+    cand = torch.where((g == best[seg]) & torch.isfinite(g), rows, torch.full_like(rows, -1))
     out = torch.full((nseg,), -1, dtype=torch.long, device=logp.device)
-    return out.scatter_reduce(0, seg[hit], rows[hit], reduce="amax", include_self=True)
+    return out.scatter_reduce(0, seg, cand, reduce="amax", include_self=True)
 
 
 class NodeEncoder(nn.Module):
-    """scheduler.py:176-245 (reverse flow: children send to parents, deepest level first)."""
+    """scheduler.py:176-245 (reverse flow: children send to parents, deepest level first). Each level runs
+    mlp_msg on every node and sums child messages into parents with the level's 0/1 edge weights: the same
+    sums as the reference's masked sparse matmul, without data-dependent shapes."""
 
     def __init__(self, num_node_features: int, embed_dim: int, mlp_kwargs: dict[str, Any]):
         super().__init__()
@@ -220,23 +234,16 @@ class NodeEncoder(nn.Module):
         if b.max_levels == 0:
             return h_init  # _forward_no_mp for every observation
         Nt = h_init.shape[0]
-        h = torch.zeros_like(h_init)
         parent, child = b.edge_index[0], b.edge_index[1]
-        has_child = torch.zeros(Nt, dtype=torch.bool, device=h.device)
-        has_child[parent] = True
-        leaf = ~has_child
-        h[leaf] = self.mlp_update(h_init[leaf])
+        ones = torch.ones(parent.numel(), dtype=h_init.dtype, device=h_init.device)
+        has_child = torch.zeros(Nt, dtype=h_init.dtype, device=h_init.device).index_add_(0, parent, ones) > 0
+        h = torch.where(has_child[:, None], torch.zeros_like(h_init), self.mlp_update(h_init))
         for lvl in range(b.max_levels - 1, -1, -1):
-            sel = ((b.edge_bits >> lvl) & 1) != 0
-            p, ch = parent[sel], child[sel]
-            src = torch.zeros(Nt, dtype=torch.bool, device=h.device)
-            src[ch] = True
-            dst = torch.zeros(Nt, dtype=torch.bool, device=h.device)
-            dst[p] = True
-            msg = torch.zeros_like(h)
-            msg[src] = self.mlp_msg(h[src])
-            agg = torch.zeros_like(h).index_add_(0, p, msg[ch])
-            h[dst] = h_init[dst] + self.mlp_update(agg[dst])
+            w = ((b.edge_bits >> lvl) & 1).to(h.dtype)
+            msg = self.mlp_msg(h)
+            agg = torch.zeros_like(h).index_add_(0, parent, msg[child] * w[:, None])
+            dst = torch.zeros(Nt, dtype=h.dtype, device=h.device).index_add_(0, parent, w) > 0
+            h = torch.where(dst[:, None], h_init + self.mlp_update(agg), h)
         if per_obs_no_mp:  # observations without message-passing levels keep h = mlp_prep(x)
             flat = (b.env_levels == 0)[b.node_env]
             h = torch.where(flat[:, None], h_init, h)
@@ -281,21 +288,25 @@ class EncoderNetwork(nn.Module):
 
 
 class StagePolicyNetwork(nn.Module):
-    """scheduler.py:284-326: one score per schedulable node (rows in flat node order)."""
+    """scheduler.py:284-326."""
 
     def __init__(self, num_node_features: int, emb_dims: dict[str, int], mlp_kwargs: dict[str, Any]):
         super().__init__()
         self.mlp_score = make_mlp(num_node_features + emb_dims["node"] + emb_dims["dag"] + emb_dims["glob"],
                                   output_dim=1, **mlp_kwargs)
 
-    def forward(self, b: DagBatch, h: dict[str, torch.Tensor]) -> torch.Tensor:
-        m = b.stage_mask
-        inp = torch.cat([b.x[m], h["node"][m], h["dag"][b.node_dag[m]], h["glob"][b.node_env[m]]], dim=1)
+    def scores_all(self, b: DagBatch, h: dict[str, torch.Tensor]) -> torch.Tensor:
+        """Score of every node row (only schedulable rows are meaningful)."""
+        inp = torch.cat([b.x, h["node"], h["dag"][b.node_dag], h["glob"][b.node_env]], dim=1)
         return self.mlp_score(inp).squeeze(-1)
+
+    def forward(self, b: DagBatch, h: dict[str, torch.Tensor]) -> torch.Tensor:
+        """The reference's output: one score per schedulable node, in flat node order."""
+        return self.scores_all(b, h)[b.stage_mask]
 
 
 class ExecPolicyNetwork(nn.Module):
-    """scheduler.py:329-385: scores of exec actions k/N, k < commit cap of the chosen DAG, per env."""
+    """scheduler.py:329-385."""
 
     def __init__(self, num_executors: int, num_dag_features: int, emb_dims: dict[str, int],
                  mlp_kwargs: dict[str, Any]):
@@ -305,19 +316,27 @@ class ExecPolicyNetwork(nn.Module):
         self.mlp_score = make_mlp(num_dag_features + emb_dims["dag"] + emb_dims["glob"] + 1, output_dim=1,
                                   **mlp_kwargs)
 
-    def forward(self, b: DagBatch, h: dict[str, torch.Tensor], dags: torch.Tensor, envs: torch.Tensor):
-        """dags/envs: i64 [K] chosen DAG (flat id) and its env per decision. Returns (scores [R], seg [R],
-        action k [R]) with R = sum of the chosen DAGs' commit caps."""
+    def scores_grid(self, b: DagBatch, h: dict[str, torch.Tensor], dags: torch.Tensor, envs: torch.Tensor):
+        """Scores of exec actions k/N for k < N, per decision (chosen DAG `dags`, its env `envs`): [K, N],
+        and the validity mask k < commit cap of the DAG (the reference's exec_mask row)."""
         N = self.num_executors
-        caps = b.exec_cap[dags].clamp(min=0, max=N)
-        seg = torch.repeat_interleave(torch.arange(dags.numel(), device=dags.device), caps)
-        start = torch.cumsum(caps, 0) - caps
-        k = torch.arange(seg.numel(), device=dags.device) - start[seg]
+        K = dags.numel()
         x_dag = b.x[b.ptr[dags], : self.num_dag_features]
-        x_h_dag = torch.cat([x_dag, h["dag"][dags]], dim=1)
-        acts = (torch.arange(N, device=dags.device) / N)[k].unsqueeze(1)
-        inp = torch.cat([x_h_dag[seg], h["glob"][envs][seg], acts], dim=1)
-        return self.mlp_score(inp).squeeze(-1), seg, k
+        base = torch.cat([x_dag, h["dag"][dags], h["glob"][envs]], dim=1)
+        acts = (torch.arange(N, device=dags.device) / N)
+        inp = torch.cat([base[:, None, :].expand(K, N, base.shape[1]), acts[None, :, None].expand(K, N, 1)], dim=2)
+        scores = self.mlp_score(inp.reshape(K * N, -1)).view(K, N)
+        valid = torch.arange(N, device=dags.device)[None, :] < b.exec_cap[dags][:, None]
+        return scores, valid
+
+    def forward(self, b: DagBatch, h: dict[str, torch.Tensor], dags: torch.Tensor, envs: torch.Tensor):
+        """The reference's output for the given decisions: scores of the valid actions (flat), their
+        decision index and action k."""
+        scores, valid = self.scores_grid(b, h, dags, envs)
+        K, N = scores.shape
+        seg = torch.arange(K, device=dags.device)[:, None].expand(K, N)
+        k = torch.arange(N, device=dags.device)[None, :].expand(K, N)
+        return scores[valid], seg[valid], k[valid]
 
 
 class DecimaScheduler(nn.Module):
@@ -347,38 +366,41 @@ class DecimaScheduler(nn.Module):
     def device(self):
         return next(self.parameters()).device
 
+    def _sched_rows(self, b: DagBatch):
+        """Per node: rank among its env's schedulable nodes (valid where stage_mask)."""
+        return torch.cumsum(b.stage_mask.long(), 0) - 1 - _excl(b.num_stage_acts)[b.node_env]
+
     @torch.no_grad()
     def schedule(self, b: DagBatch, generator=None) -> dict[str, torch.Tensor]:
         """One decision per env (envs with no schedulable stage get stage_idx -1, num_exec 1). Returns device
         tensors: stage_idx i32 [B] (index among the env's schedulable stages), num_exec i32 [B] (already
         1 + the sampled exec action, DecimaActWrapper.action), job_idx i64 [B] (DAG index within the env),
-        exec_idx i64 [B], lgprob f32 [B]."""
+        exec_idx i64 [B], lgprob f32 [B] (utils.sample: log of the softmax probability, stage + exec)."""
         B = b.num_envs
         dev = b.x.device
         h = self.encoder(b, per_obs_no_mp=True)
-        scores = self.stage_policy_network(b, h)
-        sched_env = b.node_env[b.stage_mask]
-        logp = segment_log_softmax(scores, sched_env, B)
-        pick = segment_sample(logp, sched_env, B, generator)  # flat schedulable-row index
+        scores = self.stage_policy_network.scores_all(b, h)
+        _, logp = masked_softmax_stats(scores, b.stage_mask, b.node_env, B, clamp=False)
+        pick = gumbel_pick(logp, b.node_env, B, generator)  # flat node row per env
         live = pick >= 0
-        sched_base = torch.cumsum(b.num_stage_acts, 0) - b.num_stage_acts
-        stage_idx = torch.where(live, pick - sched_base, torch.full_like(pick, -1))
-        node_rows = torch.nonzero(b.stage_mask).squeeze(1)
-        envs = torch.nonzero(live).squeeze(1)
-        dags = b.node_dag[node_rows[pick[envs]]]
-        escore, eseg, ek = self.exec_policy_network(b, h, dags, envs)
-        elogp = segment_log_softmax(escore, eseg, envs.numel())
-        epick = segment_sample(elogp, eseg, envs.numel(), generator)
-        exec_idx = torch.zeros(B, dtype=torch.long, device=dev)
-        lg = torch.zeros(B, dtype=torch.float32, device=dev)
-        job_idx = torch.full((B,), -1, dtype=torch.long, device=dev)
-        ok = epick >= 0
-        exec_idx[envs[ok]] = ek[epick[ok]]
-        lg[envs] = logp[pick[envs]]
-        lg[envs[ok]] += elogp[epick[ok]]
-        job_idx[envs] = dags - b.obs_ptr[envs]
+        row = pick.clamp(min=0)
+        stage_idx = torch.where(live, self._sched_rows(b)[row] if row.numel() and b.x.shape[0] else pick, -1)
+        envs = torch.arange(B, device=dev)
+        dags = b.node_dag[row] if b.x.shape[0] else torch.zeros(B, dtype=torch.long, device=dev)
+        es, valid = self.exec_policy_network.scores_grid(b, h, dags, envs)
+        elogp = torch.log_softmax(torch.where(valid, es, torch.full_like(es, -torch.inf)), dim=1)
+        elogp = torch.where(valid, elogp, torch.full_like(elogp, -torch.inf))
+        N = self.num_executors
+        seg = torch.arange(B, device=dev)[:, None].expand(B, N).reshape(-1)
+        epick = gumbel_pick(elogp.reshape(-1), seg, B, generator)
+        ok = live & (epick >= 0)
+        exec_idx = torch.where(ok, epick - envs * N, torch.zeros_like(epick))
+        lg_stage = torch.where(live, logp[row] if b.x.shape[0] else torch.zeros(B, device=dev),
+                               torch.zeros(B, device=dev))
+        lg_exec = torch.where(ok, elogp.reshape(-1)[epick.clamp(min=0)], torch.zeros(B, device=dev))
         return {"stage_idx": stage_idx.to(torch.int32), "num_exec": (exec_idx + 1).to(torch.int32),
-                "job_idx": job_idx, "exec_idx": exec_idx, "lgprob": lg}
+                "job_idx": torch.where(live, dags - b.obs_ptr[:-1], torch.full_like(dags, -1)),
+                "exec_idx": exec_idx, "lgprob": (lg_stage + lg_exec).float()}
 
     def evaluate_actions(self, b: DagBatch, stage_idx: torch.Tensor, job_idx: torch.Tensor,
                          exec_idx: torch.Tensor) -> dict[str, torch.Tensor]:
@@ -387,26 +409,21 @@ class DecimaScheduler(nn.Module):
         B = b.num_envs
         dev = b.x.device
         h = self.encoder(b, per_obs_no_mp=False)
-        scores = self.stage_policy_network(b, h)
-        sched_env = b.node_env[b.stage_mask]
-        s_lp, s_ent = _evaluate(scores, sched_env, B, stage_idx.long() + (torch.cumsum(b.num_stage_acts, 0)
-                                                                           - b.num_stage_acts))
+        scores = self.stage_policy_network.scores_all(b, h)
+        probs, logp = masked_softmax_stats(scores, b.stage_mask, b.node_env, B, clamp=True)
+        rows = torch.arange(b.x.shape[0], device=dev)
+        hit = b.stage_mask & (self._sched_rows(b) == stage_idx.long()[b.node_env])
+        sel = torch.full((B,), -1, dtype=torch.long, device=dev).scatter_reduce(
+            0, b.node_env, torch.where(hit, rows, torch.full_like(rows, -1)), reduce="amax", include_self=True)
+        s_lp = logp[sel.clamp(min=0)]
+        s_ent = -segment_sum(torch.where(b.stage_mask, logp * probs, torch.zeros_like(probs)), b.node_env, B)
         envs = torch.arange(B, device=dev)
         dags = job_idx.long() + b.obs_ptr[:-1]
-        escore, eseg, ek = self.exec_policy_network(b, h, dags, envs)
-        caps = b.exec_cap[dags].clamp(min=0, max=self.num_executors)
-        e_lp, e_ent = _evaluate(escore, eseg, B, exec_idx.long() + (torch.cumsum(caps, 0) - caps))
+        es, valid = self.exec_policy_network.scores_grid(b, h, dags, envs)
+        N = self.num_executors
+        seg = envs[:, None].expand(B, N).reshape(-1)
+        ep, elp = masked_softmax_stats(es.reshape(-1), valid.reshape(-1), seg, B, clamp=True)
+        e_lp = elp[envs * N + exec_idx.long()]
+        e_ent = -segment_sum(torch.where(valid.reshape(-1), elp * ep, torch.zeros_like(ep)), seg, B)
         ent = (s_ent + e_ent) / (self.num_executors * b.num_nodes).float().log()
         return {"lgprobs": s_lp + e_lp, "entropies": ent}
-
-
-def _evaluate(scores: torch.Tensor, seg: torch.Tensor, nseg: int, sel: torch.Tensor):
-    """utils.py:25-48: probs = clamp_probs(pyg softmax); log-prob of the selection, entropy per segment."""
-    eps = torch.finfo(scores.dtype).eps
-    mx = torch.full((nseg,), -torch.inf, dtype=scores.dtype, device=scores.device)
-    mx = mx.scatter_reduce(0, seg, scores.detach(), reduce="amax", include_self=True)
-    ex = torch.exp(scores - mx[seg])
-    probs = (ex / (segment_sum(ex, seg, nseg) + 1e-16)[seg]).clamp(min=eps, max=1 - eps)
-    logp = probs.log()
-    ent = -segment_sum(logp * probs, seg, nseg)
-    return logp[sel], ent
