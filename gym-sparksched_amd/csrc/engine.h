@@ -74,14 +74,40 @@ struct StepIn {
 
 // Everything a launch needs besides the arenas. Lives at the start of the state arena (device memory),
 // so kernels take one pointer and read fields through the scalar cache.
+// Executor-key table per number of local executors n (tpch.py:216-235 on executor_intervals, tpch.py:237-262):
+// {lo, hi, level(lo), level(hi)} — the interval's EXEC_LEVELS values (small integers) and their indices, so
+// the sampler's key choice is scalar-cache reads instead of two dependent dataset loads.
+constexpr int kIvRows = 256;
 struct Params {
   ssim_layout L;
   StateOffsets O;
   ssim_dataset D;
   ssim_config C;
+  uint8_t iv[kIvRows][4];
 };
 constexpr int64_t kParamsReserve = 4096;
 static_assert(sizeof(Params) <= kParamsReserve, "params block");
+
+__host__ __device__ inline int exec_level_index(double key) {  // EXEC_LEVELS index, 0xFF if not a level
+  return key == 5.0 ? 0 : key == 10.0 ? 1 : key == 20.0 ? 2 : key == 40.0 ? 3 : key == 50.0 ? 4
+         : key == 60.0 ? 5 : key == 80.0 ? 6 : key == 100.0 ? 7 : 0xFF;
+}
+
+// Host side: fill Params::iv from the packed executor_intervals table ((N+1) x 2 float64, host memory).
+// Returns false if a value is not a small integer (the table's values are EXEC_LEVELS members).
+inline bool fill_interval_table(Params* p, const double* intervals, int num_executors) {
+  memset(p->iv, 0, sizeof(p->iv));
+  for (int n = 0; n <= num_executors && n < kIvRows; ++n) {
+    const double lo = intervals[2 * n], hi = intervals[2 * n + 1];
+    if (!(lo >= 0 && lo <= 255 && hi >= 0 && hi <= 255 && lo == (double)(int)lo && hi == (double)(int)hi))
+      return false;
+    p->iv[n][0] = (uint8_t)lo;
+    p->iv[n][1] = (uint8_t)hi;
+    p->iv[n][2] = (uint8_t)exec_level_index(lo);
+    p->iv[n][3] = (uint8_t)exec_level_index(hi);
+  }
+  return true;
+}
 
 // kN / kJ: executor count and job cap as compile-time constants (0 = read from the layout at run time).
 // A specialised instantiation sees every (N, J)-dependent offset, loop bound and table size as a constant.
@@ -90,6 +116,7 @@ struct Sim {
   const ssim_layout& L;
   const ssim_dataset& D;
   const ssim_config& C;
+  const uint8_t (*IV)[4];    // Params::iv
   const int32_t NE, JC, SC;  // executors, job cap, stage cap
   const StateOffsets O;      // re-derived from (NE, JC, SC): same function as the host layout
   uint8_t* ghot;  // this env's hot block in HBM
@@ -107,7 +134,7 @@ struct Sim {
   // `lds` = this wave's LDS block: [hot copy (if resident) | scratch]; resident=false keeps hot in HBM.
   __device__ __forceinline__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* lds,
                                  uint8_t* obs_arena, int32_t env_index, bool resident)
-      : L(p->L), D(p->D), C(p->C), NE(kN ? kN : p->L.num_executors), JC(kJ ? kJ : p->L.job_cap),
+      : L(p->L), D(p->D), C(p->C), IV(p->iv), NE(kN ? kN : p->L.num_executors), JC(kJ ? kJ : p->L.job_cap),
         SC(p->L.stage_cap), O(state_offsets(NE, JC, SC)),
         ghot(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
@@ -202,6 +229,19 @@ struct Sim {
     return W::uni(ldg(q, i));
   }
 
+  // Wave-uniform register copy of a whole record for serial code: one LDS access (16-B loads) and every
+  // word through W::uni (SGPRs), instead of one dependent load per field; written back with `rec = copy`.
+  template <class R>
+  __device__ __forceinline__ R ld_rec(const R& src) const {
+    static_assert(sizeof(R) % 4 == 0, "records are whole words");
+    uint32_t w[sizeof(R) / 4];
+    __builtin_memcpy(w, &src, sizeof(R));
+    for (int i = 0; i < (int)(sizeof(R) / 4); ++i) w[i] = W::uni(w[i]);
+    R r;
+    __builtin_memcpy(&r, w, sizeof(R));
+    return r;
+  }
+
   // records (layout.h)
   __device__ __forceinline__ StageRec& stage(int g) const { return H<StageRec>(O.stages)[g]; }
   __device__ __forceinline__ JobRec& job(int j) const { return H<JobRec>(O.jobs)[j]; }
@@ -217,7 +257,7 @@ struct Sim {
   __device__ __forceinline__ UF<int16_t> st_exe(int g) const { return {&stage(g).exe}; }
   __device__ __forceinline__ UF<int16_t> st_mov(int g) const { return {&stage(g).mov}; }
   __device__ __forceinline__ UF<int16_t> st_com(int g) const { return {&stage(g).com}; }
-  __device__ __forceinline__ UF<int16_t> st_unmet(int g) const { return {&stage(g).unmet}; }
+  __device__ __forceinline__ UF<int8_t> st_unmet(int g) const { return {&stage(g).unmet}; }
   __device__ __forceinline__ UF<uint8_t> st_sel(int g) const { return {&stage(g).sel}; }
   __device__ __forceinline__ UF<double> st_recent(int g) const { return {recent() + g}; }
   __device__ __forceinline__ bool st_completed(int g) const { return st_rem(g) == 0 && st_exe(g) == 0; }
@@ -775,36 +815,30 @@ struct Sim {
     return true;
   }
 
-  __device__ __forceinline__ static int level_of(double key) {  // EXEC_LEVELS index, -1 if not a level
-    return key == 5.0 ? 0 : key == 10.0 ? 1 : key == 20.0 ? 2 : key == 40.0 ? 3 : key == 50.0 ? 4
-           : key == 60.0 ? 5 : key == 80.0 ? 6 : key == 100.0 ? 7 : -1;
-  }
-
-  __device__ __forceinline__ double task_duration(int j, int g, int e) {
-    const int n_local = job_local(j);
-    check(n_local > 0);
-    const int ts = st_ts(g);
+  // n_local = len(job.local_executors), ts = the stage's template stage, last = the executor's last task's
+  // local stage (-1 = None), lid = this stage's local id, keymask / maxlevel = the stage record's copies of
+  // the template stage's first_wave key set. The only dataset loads are the descriptor gather (issued first,
+  // independent of the RNG) and the drawn duration; the executor key comes from Params::iv (scalar cache).
+  __device__ __forceinline__ double task_duration(int n_local, int ts, int last, int lid, int keymask,
+                                                  int maxlevel) {
+    check(n_local > 0 && n_local < kIvRows);
     const DurDesc dd = dur_gather(ts);
-    const int keymask = ldu(D.ts_fw_keymask, ts), maxlevel = ldu(D.ts_fw_maxlevel, ts);
-    const double lo = ldu(D.intervals, 2 * n_local), hi = ldu(D.intervals, 2 * n_local + 1);
-    double key;
-    if (lo == hi) {
-      key = lo;
-    } else {
-      const int pt = 1 + (int)(rng.random() * (hi - lo));
-      key = ((double)pt <= (double)n_local - lo) ? lo : hi;
+    const uint32_t iv = W::uni(*reinterpret_cast<const uint32_t*>(IV[n_local < kIvRows ? n_local : 0]));
+    const int lo = (int)(iv & 0xFF), hi = (int)((iv >> 8) & 0xFF);
+    int level = (int)((iv >> 16) & 0xFF);  // key = lo
+    if (lo != hi) {  // _sample_executor_key (tpch.py:216-235): one random() draw
+      const int pt = 1 + (int)(rng.random() * (double)(hi - lo));
+      if (!(pt <= n_local - lo)) level = (int)(iv >> 24);  // key = hi
     }
-    int level = level_of(key);
-    if (level < 0 || !((keymask >> level) & 1)) level = maxlevel;
+    if (level >= kNumLevels || !((keymask >> level) & 1)) level = maxlevel;
     double d = 0.0;
-    const int last = ex_task(e);
     if (last < 0) {
       if (draw(ts, dd, 0, level, &d)) return d;
       if (draw(ts, dd, 1, level, &d)) return d + C.warmup_delay;
       fail(SSIM_ERR_SAMPLER);
       return 0.0;
     }
-    if (last == g - job_base(j)) {
+    if (last == lid) {
       if (draw(ts, dd, 2, level, &d)) return d;
     }
     if (draw(ts, dd, 1, level, &d)) return d;
@@ -888,22 +922,37 @@ struct Sim {
     ex_task(e) = -1;
   }
 
-  __device__ __forceinline__ void run_next_task(int e, int g) {  // :584-615
-    const int j = st_job(g);
-    check(st_rem(g) > 0);
-    check(ex_job(e) == j);
-    check(!ex_busy(e));
-    st_rem(g) -= 1;
-    st_exe(g) += 1;
-    if (st_rem(g) == 0) job_sat(j) += 1;
+  // _execute_next_task (:584-615) on register copies of the stage and executor records (ld_rec), which the
+  // caller writes back: the task-completion path then costs one LDS access per record, not one per field.
+  __device__ __forceinline__ void run_next_task_rec(int g, StageRec& s, ExecRec& x) {
+    const int j = s.job;
+    check(s.rem > 0);
+    check(x.job == j);
+    check(!x.busy);
+    s.rem = (int16_t)(s.rem - 1);
+    s.exe = (int16_t)(s.exe + 1);
+    const JobRec jr = ld_rec(job(j));
+    if (s.rem == 0) job_sat(j) = (int16_t)(jr.sat + 1);
     SSIM_TIC(t_smp);
     SSIM_COUNT(kCtTask);
-    const double dur = task_duration(j, g, e);
+    const int lid = g - jr.base;
+    const double dur = task_duration(jr.local, s.ts, x.task, lid, s.fw_keymask, s.fw_maxlevel);
     SSIM_TOC(t_smp, kPhSample);
-    ex_task(e) = (int16_t)(g - job_base(j));
-    ex_busy(e) = 1;
+    x.task = (int16_t)lid;
+    x.busy = 1;
     st_recent(g) = dur;
-    push_event(e, h.wall + dur, kEvTask, g);
+    check(x.ev_seq < 0);  // at most one pending event per executor
+    x.ev_t = h.wall + dur;
+    x.ev_seq = h.seq++;
+    x.ev_type = (int16_t)kEvTask;
+    x.ev_stage = (int16_t)g;
+  }
+  __device__ __forceinline__ void run_next_task(int e, int g) {  // :584-615
+    StageRec s = ld_rec(stage(g));
+    ExecRec x = ld_rec(exr(e));
+    run_next_task_rec(g, s, x);
+    stage(g) = s;
+    exr(e) = x;
   }
 
   __device__ __forceinline__ void send(int e, int g) {  // :617-637
@@ -1078,14 +1127,20 @@ struct Sim {
   }
 
   __device__ __forceinline__ void on_task_done(int e, int g) {  // :452-483
-    const int j = st_job(g);
-    check(!st_completed(g));
-    st_exe(g) -= 1;
-    ex_busy(e) = 0;
-    if (st_rem(g) > 0) {
-      run_next_task(e, g);
+    StageRec s = ld_rec(stage(g));
+    ExecRec x = ld_rec(exr(e));
+    const int j = s.job;
+    check(!(s.rem == 0 && s.exe == 0));
+    s.exe = (int16_t)(s.exe - 1);
+    x.busy = 0;
+    if (s.rem > 0) {  // the common case: the executor takes the stage's next task
+      run_next_task_rec(g, s, x);
+      stage(g) = s;
+      exr(e) = x;
       return;
     }
+    stage(g) = s;
+    exr(e) = x;
     bool changed = false;
     if (st_completed(g)) changed = stage_completed(j, g);
     if (job_nact(j) == 0) job_completed(j);
@@ -1596,8 +1651,10 @@ struct Sim {
           st_exe(g) = 0;
           st_mov(g) = 0;
           st_com(g) = 0;
-          st_unmet(g) = (int16_t)(ldg(D.ts_parent_base, ts + 1) - ldg(D.ts_parent_base, ts));
+          st_unmet(g) = (int8_t)(ldg(D.ts_parent_base, ts + 1) - ldg(D.ts_parent_base, ts));
           st_sel(g) = 0;
+          stage(g).fw_keymask = (uint8_t)ldg(D.ts_fw_keymask, ts);
+          stage(g).fw_maxlevel = (uint8_t)ldg(D.ts_fw_maxlevel, ts);
           st_recent(g) = ldg(D.ts_rough, ts);
         }
       }

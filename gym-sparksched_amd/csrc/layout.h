@@ -58,8 +58,10 @@ struct StageRec {
   int16_t job, ts;       // owning job, template-stage index into the dataset
   int16_t rem, exe;      // Stage.num_remaining_tasks / num_executing_tasks (stage.py:5-18)
   int16_t mov, com;      // ExecutorTracker moving-to / commitments-to this stage
-  int16_t unmet;         // parents not yet completed (frontier <=> unmet == 0, job.py:93-128)
-  uint8_t sel, pad;      // selected in the current round (spark_sched_sim.py:304)
+  int8_t unmet;          // parents not yet completed (frontier <=> unmet == 0, job.py:93-128)
+  uint8_t sel;           // selected in the current round (spark_sched_sim.py:304)
+  uint8_t fw_keymask;    // sampler (copied from the dataset at reset): bit l <=> EXEC_LEVELS[l] is a
+  uint8_t fw_maxlevel;   //   first_wave key; level index of max(first_wave) (tpch.py:216-235)
 };
 static_assert(sizeof(StageRec) == 16, "stage record");
 
@@ -200,7 +202,8 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
 // Computes the public layout and the private offsets. Returns false on a bad / unsupported config.
 inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets* O) {
   if (cfg.num_envs <= 0 || cfg.num_executors <= 0 || cfg.num_executors > 250 || cfg.job_cap <= 0 ||
-      cfg.max_stages <= 0 || cfg.max_stages > 255 || cfg.max_edges < 0 || cfg.trace_cap < 0)
+      cfg.max_stages <= 0 || cfg.max_stages > 128 /* int8 parent countdown */ || cfg.max_edges < 0 ||
+      cfg.trace_cap < 0)
     return false;
   memset(L, 0, sizeof(*L));
   const int64_t B = cfg.num_envs, N = cfg.num_executors, J = cfg.job_cap;

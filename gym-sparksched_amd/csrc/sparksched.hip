@@ -212,6 +212,19 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
   h->state = static_cast<uint8_t*>(state_arena);
   h->obs = static_cast<uint8_t*>(obs_arena);
   h->reset = static_cast<uint8_t*>(reset_arena);
+  {  // executor-key table for the sampler, from the dataset's executor_intervals
+    const int N = cfg->num_executors;
+    double* iv = new double[2 * (N + 1)];
+    int rc0 = hip_check(hipMemcpy(iv, dataset->intervals, sizeof(double) * 2 * (N + 1), hipMemcpyDeviceToHost),
+                        "intervals download");
+    if (rc0 == SSIM_OK && !fill_interval_table(&h->params, iv, N))
+      rc0 = set_err(SSIM_E_ARG, "ssim_create: executor_intervals values are not EXEC_LEVELS integers");
+    delete[] iv;
+    if (rc0 != SSIM_OK) {
+      delete h;
+      return rc0;
+    }
+  }
   int rc = hip_check(hipMemcpy(h->state, &h->params, sizeof(Params), hipMemcpyHostToDevice), "params upload");
   if (rc == SSIM_OK) rc = hip_check(hipMemset(h->obs, 0, (size_t)h->params.L.obs_bytes), "obs clear");
   if (rc == SSIM_OK)

@@ -20,6 +20,7 @@ struct WaveHip {
   __device__ static __forceinline__ int16_t uni(int16_t v) { return (int16_t)__builtin_amdgcn_readfirstlane((int)v); }
   __device__ static __forceinline__ uint16_t uni(uint16_t v) { return (uint16_t)__builtin_amdgcn_readfirstlane((int)v); }
   __device__ static __forceinline__ uint8_t uni(uint8_t v) { return (uint8_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ static __forceinline__ int8_t uni(int8_t v) { return (int8_t)__builtin_amdgcn_readfirstlane((int)v); }
   __device__ static __forceinline__ uint64_t uni(uint64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));

@@ -79,6 +79,10 @@ int hs_create(const ssim_config* cfg, const ssim_dataset* ds, hs_handle** out, s
   }
   p.D = *ds;
   p.C = *cfg;
+  if (!fill_interval_table(&p, ds->intervals, cfg->num_executors)) {
+    free(h);
+    return -2;
+  }
   h->state = (uint8_t*)calloc(1, (size_t)p.L.state_bytes);
   h->obs = (uint8_t*)calloc(1, (size_t)p.L.obs_bytes);
   h->reset = (uint8_t*)calloc(1, (size_t)p.L.reset_bytes);
