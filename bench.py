@@ -185,6 +185,8 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--torch-policy", action="store_true",
+                    help="decima workload: run the PyTorch DecimaScheduler instead of the fused kernel")
     ap.add_argument("--ppo-time-limit", type=float, default=0.0,
                     help="ppo workload: override mean_time_limit (ms) of config/decima_tpch.yaml (0 = keep 2e7)")
     ap.add_argument("--no-autoreset", action="store_true",
@@ -248,8 +250,11 @@ def main():
                     events[2 * k + 1].record(stream)
         elif args.mode == "decima":
             for k in range(n):
-                b = build_batch(eng.views, eng.decima_features())
-                act = pol.schedule(b, generator=gen)
+                if args.torch_policy:  # the batched PyTorch module (~150 launches per decision)
+                    act = pol.schedule(build_batch(eng.views, eng.decima_features()), generator=gen)
+                else:  # one fused HIP launch (ssim_decima_policy)
+                    run.counter += 1
+                    act = pol.schedule_fused(eng, eng.decima_features(), seed=args.seed, counter=run.counter)
                 if events is not None:
                     events[2 * k].record(stream)
                 eng.step(act["stage_idx"], act["num_exec"])
@@ -330,6 +335,8 @@ def main():
             "config": {"workload": wl["desc"].format(B=B), "envs_per_gpu": B,
                        "jobs": cfg["job_arrival_cap"], "executors": cfg["num_executors"],
                        "mean_time_limit": wl["mean_time_limit"], "mode": args.mode,
+                       "policy": ("torch" if args.torch_policy else "fused HIP kernel") if args.mode == "decima"
+                       else "device random",
                        "steps_per_launch": chunk if args.mode == "rollout" else 1,
                        "autoreset": bool(args.mode != "step" and (flags or args.mode == "decima")),
                        "parallelism": f"env-sharded x{world}"},

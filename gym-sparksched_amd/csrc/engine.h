@@ -936,7 +936,9 @@ struct Sim {
     SSIM_TIC(t_smp);
     SSIM_COUNT(kCtTask);
     const int lid = g - jr.base;
+    SSIM_MARK("sample_begin");
     const double dur = task_duration(jr.local, s.ts, x.task, lid, s.fw_keymask, s.fw_maxlevel);
+    SSIM_MARK("sample_end");
     SSIM_TOC(t_smp, kPhSample);
     x.task = (int16_t)lid;
     x.busy = 1;
@@ -1127,6 +1129,7 @@ struct Sim {
   }
 
   __device__ __forceinline__ void on_task_done(int e, int g) {  // :452-483
+    SSIM_MARK("task_done_begin");
     StageRec s = ld_rec(stage(g));
     ExecRec x = ld_rec(exr(e));
     const int j = s.job;

@@ -15,6 +15,7 @@
 #include "sparksched.h"
 #include "engine.h"
 #include "decima.h"
+#include "decima_policy.h"
 #include "policy.h"
 #include "wave_hip.h"
 
@@ -125,6 +126,29 @@ __global__ __launch_bounds__(64) void k_decima(const Params* __restrict__ P, con
                                                int32_t* depth) {
   DecimaView<WaveHip> v{P->L, obs, (int)blockIdx.x};
   v.run(nts, ws, g_smem, feats, ccap, emask, depth);
+}
+
+__global__ __launch_bounds__(64) void k_decima_policy(const Params* __restrict__ P, const uint8_t* __restrict__ obs,
+                                                      const float* __restrict__ feats, const int32_t* __restrict__ ccap,
+                                                      const uint32_t* __restrict__ emask,
+                                                      const int32_t* __restrict__ depth, const float* __restrict__ Wt,
+                                                      int node_cap, uint64_t seed, uint64_t counter,
+                                                      const uint8_t* __restrict__ env_mask, DecimaPolicyOut o,
+                                                      int32_t* overflow) {
+  const int eid = blockIdx.x;
+  if (env_mask != nullptr && env_mask[eid] == 0) {
+    if (WaveHip::lane() == 0) {
+      o.stage_idx[eid] = -1;
+      o.num_exec[eid] = 1;
+      o.job_idx[eid] = -1;
+      o.exec_idx[eid] = 0;
+      o.lgprob[eid] = 0.0f;
+    }
+    return;
+  }
+  if (!decima_policy_env(P, obs, feats, ccap, emask, depth, Wt, node_cap, seed, counter, eid, g_smem, o) &&
+      WaveHip::lane() == 0 && overflow != nullptr)
+    atomicAdd(overflow, 1);
 }
 
 // per-job arrival/completion times and state (JobRec/JobTimes in the hot block) -> [num_envs][job_cap]
@@ -335,6 +359,42 @@ extern "C" int ssim_decima_features(ssim_handle* h, float num_tasks_scale, float
   hipLaunchKernelGGL(k_decima, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream, dparams(h), h->obs,
                      num_tasks_scale, work_scale, node_feats, commit_cap, edge_mask, depth);
   return hip_check(hipGetLastError(), "k_decima launch");
+}
+
+extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const int32_t* commit_cap,
+                                  const uint32_t* edge_mask, const int32_t* depth, const float* params,
+                                  int32_t num_params, int32_t node_cap, uint64_t seed, uint64_t counter,
+                                  const uint8_t* env_mask, int32_t* stage_idx, int32_t* num_exec, int32_t* job_idx,
+                                  int32_t* exec_idx, float* lgprob, float* stage_scores, float* exec_scores,
+                                  int32_t* overflow, void* stream) {
+  if (h == nullptr || node_feats == nullptr || commit_cap == nullptr || edge_mask == nullptr || depth == nullptr ||
+      params == nullptr || stage_idx == nullptr || num_exec == nullptr || job_idx == nullptr ||
+      exec_idx == nullptr || lgprob == nullptr)
+    return set_err(SSIM_E_ARG, "ssim_decima_policy: null argument");
+  if (num_params != kDecimaParams)
+    return set_err(SSIM_E_ARG, "ssim_decima_policy: %d parameters, the fused kernel implements the "
+                   "decima_tpch.yaml architecture (%d)", num_params, kDecimaParams);
+  const ssim_layout& L = h->params.L;
+  if (L.num_executors > 64 * kDpExecChunks)
+    return set_err(SSIM_E_ARG, "ssim_decima_policy: more than %d executors", 64 * kDpExecChunks);
+  if (node_cap <= 0 || node_cap > L.stage_cap) node_cap = L.stage_cap;
+  if (node_cap < (L.num_executors + kDpEmb - 1) / kDpEmb) node_cap = (L.num_executors + kDpEmb - 1) / kDpEmb;
+  const int64_t lds = decima_policy_lds_bytes(node_cap, L.job_cap);
+  if (lds > kDecimaPolicyLdsMax)
+    return set_err(SSIM_E_ARG, "ssim_decima_policy: node_cap %d needs %lld B of LDS (max %lld)", node_cap,
+                   (long long)lds, (long long)kDecimaPolicyLdsMax);
+  static int64_t configured = 0;
+  if (lds > 64 * 1024 && lds > configured) {
+    int rc = hip_check(hipFuncSetAttribute((const void*)k_decima_policy, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds), "k_decima_policy LDS attribute");
+    if (rc != SSIM_OK) return rc;
+    configured = lds;
+  }
+  DecimaPolicyOut o{stage_idx, num_exec, job_idx, exec_idx, lgprob, stage_scores, exec_scores};
+  hipLaunchKernelGGL(k_decima_policy, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream, dparams(h),
+                     h->obs, node_feats, commit_cap, edge_mask, depth, params, node_cap, seed, counter, env_mask, o,
+                     overflow);
+  return hip_check(hipGetLastError(), "k_decima_policy launch");
 }
 
 extern "C" const char* ssim_last_error(void) { return g_err; }

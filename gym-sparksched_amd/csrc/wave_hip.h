@@ -150,6 +150,19 @@ struct WaveHip {
   __device__ static __forceinline__ void amax(int* p, int v) { atomicMax(p, v); }
   __device__ static __forceinline__ void amin(int* p, int v) { atomicMin(p, v); }
   __device__ static __forceinline__ void aor(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+  __device__ static __forceinline__ float max_f(float x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float y = __shfl_xor(x, off);
+      x = y > x ? y : x;
+    }
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+  }
+  __device__ static __forceinline__ float sum_f(float x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+  }
   __device__ static __forceinline__ int max_i(int x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

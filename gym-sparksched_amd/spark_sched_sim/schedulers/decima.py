@@ -39,6 +39,7 @@ from .. import _abi
 
 NUM_NODE_FEATURES = 5  # env_wrapper.py:9
 NUM_DAG_FEATURES = 3   # scheduler.py:34
+DECIMA_PARAMS = 20802  # parameters of the decima_tpch.yaml architecture (the fused kernel's; csrc/decima_policy.h)
 
 
 def make_mlp(input_dim: int, hid_dims: list[int], output_dim: int, act_cls: str,
@@ -401,6 +402,50 @@ class DecimaScheduler(nn.Module):
         return {"stage_idx": stage_idx.to(torch.int32), "num_exec": (exec_idx + 1).to(torch.int32),
                 "job_idx": torch.where(live, dags - b.obs_ptr[:-1], torch.full_like(dags, -1)),
                 "exec_idx": exec_idx, "lgprob": (lg_stage + lg_exec).float()}
+
+    @torch.no_grad()
+    def schedule_fused(self, engine, feats: dict | None = None, seed: int = 0, counter: int = 0,
+                       env_mask: torch.Tensor | None = None, node_cap: int | None = None,
+                       with_scores: bool = False) -> dict[str, torch.Tensor]:
+        """`schedule` for every env of a DeviceEngine in ONE kernel launch (ssim_decima_policy,
+        csrc/decima_policy.h): the same forward over the obs arena and the device features, weights read
+        from a packed copy of this module's parameters, sampling on a counter-based device stream of
+        (seed, env, counter). Only the decima_tpch.yaml architecture (20802 parameters). Returns the same keys
+        as `schedule` (int32/float32 device tensors); with_scores adds per-env stage scores [B, stage_cap]
+        and exec scores [B, N]."""
+        from .. import native
+
+        eng = engine
+        L = eng.layout
+        B = eng.num_envs
+        dev = eng.device
+        if feats is None:
+            feats = eng.decima_features()
+        params = torch.cat([p.detach().reshape(-1).float() for p in self.parameters()]).to(dev).contiguous()
+        if node_cap is None:
+            node_cap = int(eng.views["counts"][:, _abi.OC_NUM_NODES].max().item())
+        i32 = dict(dtype=torch.int32, device=dev)
+        out = {"stage_idx": torch.empty(B, **i32), "num_exec": torch.empty(B, **i32),
+               "job_idx": torch.empty(B, **i32), "exec_idx": torch.empty(B, **i32),
+               "lgprob": torch.empty(B, dtype=torch.float32, device=dev)}
+        ss = es = None
+        if with_scores:
+            ss = torch.full((B, L.stage_cap), float("nan"), dtype=torch.float32, device=dev)
+            es = torch.full((B, L.num_executors), float("nan"), dtype=torch.float32, device=dev)
+        overflow = torch.zeros(1, **i32)
+        m = None if env_mask is None else env_mask.to(device=dev, dtype=torch.uint8).contiguous()
+        native.check(native.lib().ssim_decima_policy(
+            eng.handle, feats["node_feats"].data_ptr(), feats["commit_cap"].data_ptr(), feats["edge_mask"].data_ptr(),
+            feats["depth"].data_ptr(), params.data_ptr(), params.numel(), max(node_cap, 1), seed, counter,
+            None if m is None else m.data_ptr(), out["stage_idx"].data_ptr(), out["num_exec"].data_ptr(),
+            out["job_idx"].data_ptr(), out["exec_idx"].data_ptr(), out["lgprob"].data_ptr(),
+            None if ss is None else ss.data_ptr(), None if es is None else es.data_ptr(), overflow.data_ptr(),
+            eng._stream()), "ssim_decima_policy")
+        self._keep = (params, m)
+        out["overflow"] = overflow
+        if with_scores:
+            out["stage_scores"], out["exec_scores"] = ss, es
+        return out
 
     def evaluate_actions(self, b: DagBatch, stage_idx: torch.Tensor, job_idx: torch.Tensor,
                          exec_idx: torch.Tensor) -> dict[str, torch.Tensor]:

@@ -88,7 +88,7 @@ class PPO:
             def engine_factory(cfg, n, ds):
                 return DeviceEngine(cfg, n, ds, device=self.device)
         self.engine = engine_factory({k: v for k, v in env_cfg.items() if k != "mean_time_limit"}, B, dataset)
-        self.collector = RolloutCollector(self.engine, self.scheduler)
+        self.collector = RolloutCollector(self.engine, self.scheduler, seed=self.seed * 7919 + self.rank)
         self.gen = torch.Generator(device=self.device).manual_seed(self.seed * 7919 + self.rank)
         self.time_limit_rngs = None
         if self.mean_time_limit:

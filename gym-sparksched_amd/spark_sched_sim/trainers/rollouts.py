@@ -79,10 +79,17 @@ class GpuRolloutBuffer:
 class RolloutCollector:
     """Drives a DeviceEngine (or the test-only HostEngine) with a DecimaScheduler until every env is done."""
 
-    def __init__(self, engine, policy, num_tasks_scale: float = 200.0, work_scale: float = 1e5):
+    def __init__(self, engine, policy, num_tasks_scale: float = 200.0, work_scale: float = 1e5, fused: bool = True,
+                 seed: int = 0):
         self.engine = engine
         self.policy = policy
         self.scales = (num_tasks_scale, work_scale)
+        from ..schedulers.decima import DECIMA_PARAMS
+
+        # the fused kernel implements the decima_tpch.yaml architecture only
+        self.fused = fused and sum(p.numel() for p in policy.parameters()) == DECIMA_PARAMS
+        self.seed = seed
+        self.counter = 0
         self.on_device = isinstance(engine.views["counts"], torch.Tensor)  # DeviceEngine vs test host build
 
     def _views(self, features: bool = True):
@@ -113,7 +120,14 @@ class RolloutCollector:
                 break
             v, f = self._views()
             b_all = build_batch(v, f, env_mask=alive)
-            act = self.policy.schedule(b_all, generator=generator)
+            if self.on_device and self.fused:  # one fused kernel launch (ssim_decima_policy)
+                self.counter += 1
+                fo = self.policy.schedule_fused(eng, f, seed=self.seed, counter=self.counter, env_mask=alive,
+                                                node_cap=int(b_all.num_nodes.max().item()))
+                act = {"stage_idx": fo["stage_idx"], "num_exec": fo["num_exec"], "job_idx": fo["job_idx"].long(),
+                       "exec_idx": fo["exec_idx"].long(), "lgprob": fo["lgprob"]}
+            else:
+                act = self.policy.schedule(b_all, generator=generator)
             envs = torch.nonzero(alive).squeeze(1)
             batch = select_envs(b_all, envs)
             si = torch.where(alive, act["stage_idx"], torch.full_like(act["stage_idx"], -2))

@@ -202,6 +202,23 @@ int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32
 int ssim_decima_features(ssim_handle* h, float num_tasks_scale, float work_scale, float* node_feats,
                          int32_t* commit_cap, uint32_t* edge_mask, int32_t* depth, void* stream);
 
+/* Fused Decima policy (schedulers/decima/scheduler.py:70-101 DecimaScheduler.schedule) for the
+ * decima_tpch.yaml architecture (embed 16, GNN MLPs [32,16] LeakyReLU(0.2), policy MLPs [64,64] Tanh;
+ * num_params must be 20802): one launch encodes every env's DAG batch from the obs arena and the
+ * ssim_decima_features outputs, scores the schedulable stages and the exec actions, and samples both
+ * (Gumbel-max on a counter-based stream of (seed, env, counter)). `params`: fp32 device buffer, the
+ * module's parameters in DecimaScheduler.parameters() order (torch nn.Linear layout). `node_cap`: LDS
+ * plan (>= the largest env's node count; 0 = stage_cap); envs above it are skipped and counted in
+ * `overflow` (device int32, optional). env_mask (optional uint8 [B]): 0 = skip the env.
+ * Outputs [B]: stage_idx (index among schedulable stages, -1 none), num_exec (= 1 + exec_idx), job_idx
+ * (active-job index), exec_idx, lgprob (log-probability of both choices); optional stage_scores
+ * [B][stage_cap] and exec_scores [B][N] (for checking). */
+int ssim_decima_policy(ssim_handle* h, const float* node_feats, const int32_t* commit_cap, const uint32_t* edge_mask,
+                       const int32_t* depth, const float* params, int32_t num_params, int32_t node_cap, uint64_t seed,
+                       uint64_t counter, const uint8_t* env_mask, int32_t* stage_idx, int32_t* num_exec,
+                       int32_t* job_idx, int32_t* exec_idx, float* lgprob, float* stage_scores, float* exec_scores,
+                       int32_t* overflow, void* stream);
+
 const char* ssim_last_error(void);
 
 #ifdef __cplusplus

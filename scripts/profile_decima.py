@@ -48,6 +48,17 @@ def main():
                     tm[k] += v
         print(B, "envs:", {k: f"{v / n * 1e3:.2f} ms" for k, v in tm.items()}, "nodes", b.x.shape[0],
               "levels", b.max_levels, flush=True)
+        tf = 0.0
+        for it in range(n + 5):  # fused kernel path (ssim_decima_policy)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fo = pol.schedule_fused(eng, eng.decima_features(), seed=1, counter=it)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            eng.step(fo["stage_idx"], fo["num_exec"])
+            if it >= 5:
+                tf += t1 - t0
+        print(B, "envs: fused features+schedule", f"{tf / n * 1e3:.2f} ms", flush=True)
         with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
                                                 torch.profiler.ProfilerActivity.CUDA]) as prof:
             for _ in range(3):

@@ -407,3 +407,58 @@ def case_decima_schedule_runs(make, dataset, env_cfg, B=16, steps=30, device="cp
         eng.step(act["stage_idx"].cpu().numpy(), act["num_exec"].cpu().numpy())
         c = eng.host_views()["counts"]
         assert int(np.count_nonzero(np.asarray(c)[:, _abi.OC_ERR])) == 0
+
+
+def case_decima_fused(make, dataset, env_cfg, cfg_over, B, seed0, iters=12, device="cuda:0"):
+    """ssim_decima_policy (one fused kernel) vs the PyTorch DecimaScheduler on the same device observations:
+    stage scores of every schedulable node, exec scores of the sampled DAG, and the log-probability of the
+    sampled action, within fp32 rounding; the sampled actions are valid env actions."""
+    import torch
+
+    from spark_sched_sim.schedulers.decima import DecimaScheduler, build_batch
+
+    cfg = dict(env_cfg, **cfg_over)
+    N = cfg["num_executors"]
+    eng = make(cfg, B, dataset, 0)
+    eng.reset(seeds=[seed0 + i for i in range(B)])
+    torch.manual_seed(seed0)
+    pol = DecimaScheduler(N).to(device)
+    for p in pol.parameters():
+        p.data.add_(0.05 * torch.randn_like(p))
+    checked = 0
+    for it in range(iters):
+        feats = eng.decima_features()
+        b = build_batch(eng.views, feats)
+        with torch.no_grad():
+            h = pol.encoder(b, per_obs_no_mp=True)
+            ref = pol.stage_policy_network.scores_all(b, h)
+        fo = pol.schedule_fused(eng, feats, seed=7, counter=it, with_scores=True)
+        assert int(fo["overflow"].item()) == 0
+        si, ji, ei = fo["stage_idx"].cpu(), fo["job_idx"].cpu(), fo["exec_idx"].cpu()
+        ss, lg = fo["stage_scores"].cpu(), fo["lgprob"].cpu()
+        node_env, mask = b.node_env.cpu(), b.stage_mask.cpu()
+        refc = ref.cpu()
+        for e in range(B):
+            rows = torch.nonzero((node_env == e) & mask).squeeze(1)
+            if rows.numel() == 0:
+                assert int(si[e]) == -1
+                continue
+            local = rows - int((node_env < e).sum())
+            got = ss[e, local]
+            assert torch.allclose(got, refc[rows], rtol=1e-4, atol=1e-5), f"env{e} it{it} stage scores"
+            assert 0 <= int(si[e]) < rows.numel()
+            dag = int(b.obs_ptr[e]) + int(ji[e])
+            with torch.no_grad():
+                es, valid = pol.exec_policy_network.scores_grid(b, h, torch.tensor([dag], device=device),
+                                                                torch.tensor([e], device=device))
+            cap = int(valid.sum())
+            assert torch.allclose(fo["exec_scores"][e, :cap].cpu(), es[0, :cap].cpu(), rtol=1e-4, atol=1e-5)
+            want = (torch.log_softmax(refc[rows], 0)[int(si[e])]
+                    + torch.log_softmax(es[0, :cap].cpu(), 0)[int(ei[e])])
+            assert abs(float(lg[e]) - float(want)) <= 1e-4 + 1e-4 * abs(float(want)), f"env{e} lgprob"
+            checked += 1
+        eng.step(fo["stage_idx"], fo["num_exec"])
+        c = eng.host_views()["counts"]
+        assert int(np.count_nonzero(np.asarray(c)[:, _abi.OC_ERR])) == 0
+        eng.rollout(_abi.SSIM_POLICY_RANDOM, 3 + it, 4)
+    assert checked > B * iters // 2

@@ -45,3 +45,14 @@ def test_decima_schedule_gpu(gpu_device, dataset, env_cfg):
         return DeviceEngine(cfg, B, ds, device=gpu_device, trace_cap=trace_cap)
 
     cases.case_decima_schedule_runs(make, dataset, env_cfg, B=64, steps=50, device=gpu_device)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_over,B,seed0,every", cases.POLICY_CONFIGS)
+def test_decima_fused_kernel_gpu(gpu_device, dataset, env_cfg, cfg_over, B, seed0, every):
+    from spark_sched_sim.engine import DeviceEngine
+
+    def make(cfg, B, ds, trace_cap):
+        return DeviceEngine(cfg, B, ds, device=gpu_device, trace_cap=trace_cap)
+
+    cases.case_decima_fused(make, dataset, env_cfg, cfg_over, 32, seed0, device=gpu_device)
