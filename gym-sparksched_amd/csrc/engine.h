@@ -109,9 +109,10 @@ inline bool fill_interval_table(Params* p, const double* intervals, int num_exec
   return true;
 }
 
-// kN / kJ: executor count and job cap as compile-time constants (0 = read from the layout at run time).
-// A specialised instantiation sees every (N, J)-dependent offset, loop bound and table size as a constant.
-template <class W, int kN = 0, int kJ = 0>
+// kN / kJ / kS: executor count, job cap and stage cap as compile-time constants (0 = read from the layout at
+// run time). A fully specialised instantiation sees every section offset (hot block, scratch), loop bound
+// and table size as a constant, so LDS accesses use immediate offsets and no SGPRs hold offsets.
+template <class W, int kN = 0, int kJ = 0, int kS = 0>
 struct Sim {
   const ssim_layout& L;
   const ssim_dataset& D;
@@ -135,7 +136,7 @@ struct Sim {
   __device__ __forceinline__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* lds,
                                  uint8_t* obs_arena, int32_t env_index, bool resident)
       : L(p->L), D(p->D), C(p->C), IV(p->iv), NE(kN ? kN : p->L.num_executors), JC(kJ ? kJ : p->L.job_cap),
-        SC(p->L.stage_cap), O(state_offsets(NE, JC, SC)),
+        SC(kS ? kS : p->L.stage_cap), O(state_offsets(NE, JC, SC)),
         ghot(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         cold(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes + O.hot_bytes),
@@ -1381,19 +1382,21 @@ struct Sim {
     h.n_sched = nsched;
     h.src_idx = src_idx;
     h.stage_idx_n = n + 1;
-    h.acc_nodes += n;
-    h.acc_edges += ne;
-    h.acc_jobs += nj;
-    h.acc_events += h.step_events;
+    EnvAcc a = ld_rec(*H<EnvAcc>(O.acc));
+    a.nodes += n;
+    a.edges += ne;
+    a.jobs += nj;
+    a.events += h.step_events;
+    *H<EnvAcc>(O.acc) = a;
     W::sync();
     if (W::lane() == 0) {
       int64_t* acc = reinterpret_cast<int64_t*>(obs + L.ob_acc) + (int64_t)eid * kNumAcc;
-      acc[0] = h.acc_nodes;
-      acc[1] = h.acc_edges;
-      acc[2] = h.acc_jobs;
-      acc[3] = h.acc_events;
-      acc[4] = h.acc_decisions;
-      acc[5] = h.acc_episodes;
+      acc[0] = a.nodes;
+      acc[1] = a.edges;
+      acc[2] = a.jobs;
+      acc[3] = a.events;
+      acc[4] = a.decisions;
+      acc[5] = a.episodes;
       acc[6] = 0;
       acc[7] = 0;
       int32_t* cnts = reinterpret_cast<int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
@@ -1471,7 +1474,10 @@ struct Sim {
       W::sync();
     }
     h.decisions++;
-    h.acc_decisions++;
+    {
+      UF<int64_t> d{&H<EnvAcc>(O.acc)->decisions};
+      d = (int64_t)d + 1;
+    }
     h.step_events = 0;
     SSIM_TOC(t_act, kPhAction);
     SSIM_TIC(t_rc);
@@ -1575,18 +1581,12 @@ struct Sim {
     if (nj <= 0) return;
     const EnvHeader* prev = H<EnvHeader>(O.hdr);
     const int prev_episode = W::uni(prev->episode);
-    const int64_t a_nodes = W::uni(prev->acc_nodes), a_edges = W::uni(prev->acc_edges),
-                  a_jobs = W::uni(prev->acc_jobs), a_events = W::uni(prev->acc_events),
-                  a_dec = W::uni(prev->acc_decisions),
-                  a_eps = W::uni(prev->acc_episodes) + (W::uni(prev->num_jobs) > 0 ? 1 : 0);
+    if (W::uni(prev->num_jobs) > 0) {  // the previous episode ends here (accumulators persist, EnvAcc)
+      UF<int64_t> eps{&H<EnvAcc>(O.acc)->episodes};
+      eps = (int64_t)eps + 1;
+    }
     h = EnvHeader();
     h.episode = prev_episode + 1;
-    h.acc_nodes = a_nodes;
-    h.acc_edges = a_edges;
-    h.acc_jobs = a_jobs;
-    h.acc_events = a_events;
-    h.acc_decisions = a_dec;
-    h.acc_episodes = a_eps;
     h.time_limit = rec->time_limit;
     rng.s_hi = rec->rng_state_hi;
     rng.s_lo = rec->rng_state_lo;

@@ -46,11 +46,15 @@ struct EnvHeader {
   int32_t step_events;
   int32_t src_idx;        // obs source_job_idx at the last observation
   int32_t pad[2];
-  // running sums over observations (SURVEY.md §8d algorithmic-byte accounting), kept across resets;
-  // decisions and finished episodes as well (the per-episode counters above restart at reset)
-  int64_t acc_nodes, acc_edges, acc_jobs, acc_events, acc_decisions, acc_episodes;
 };
 static_assert(sizeof(EnvHeader) % 16 == 0, "header must keep 16-B alignment");
+
+// Running sums over observations (SURVEY.md §8d algorithmic-byte accounting), decisions and finished
+// episodes, kept across resets. Updated in place once per decision, never held in registers.
+struct EnvAcc {
+  int64_t nodes, edges, jobs, events, decisions, episodes, pad[2];
+};
+static_assert(sizeof(EnvAcc) % 16 == 0, "accumulator record");
 
 // One stage (env-global index g = job base + local stage id). `done` is derived: rem + exe + done = tasks,
 // so completed <=> rem == 0 && exe == 0.
@@ -125,7 +129,8 @@ struct StateOffsets {
   int64_t hot_bytes, cold_bytes, scratch_bytes, env_bytes;
   int64_t lds_bytes;        // scratch (+ hot when LDS-resident); decided by compute_layout
   int32_t lds_resident, pad;
-  int64_t hdr, jobs, jtimes, active_jobs, picks, execs, sel_list, commits, stages, pools, active_stages, sched_list;
+  int64_t hdr, acc, jobs, jtimes, active_jobs, picks, execs, sel_list, commits, stages, pools, active_stages,
+      sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/;
   int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
       sc_row_of /*int16[S]*/;
@@ -148,6 +153,8 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   int64_t o = 0;
   O.hdr = o;
   o = align16(o + (int64_t)sizeof(EnvHeader));
+  O.acc = o;
+  o = align16(o + (int64_t)sizeof(EnvAcc));
   O.jobs = o;
   o = align16(o + (int64_t)sizeof(JobRec) * J);
   O.jtimes = o;

@@ -54,13 +54,13 @@ __global__ __launch_bounds__(64) void k_reset_sampled(const Params* __restrict__
 
 // kRes: hot block LDS-resident. A compile-time flag (not a runtime select between an LDS and an HBM pointer)
 // so every hot-block access compiles to ds_read/ds_write rather than FLAT instructions.
-template <bool kRes, int kN, int kJ>
+template <bool kRes, int kN, int kJ, int kS>
 __global__ __launch_bounds__(64) void k_step(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                              const int32_t* __restrict__ stage_idx,
                                              const int32_t* __restrict__ num_exec) {
   const int eid = blockIdx.x;
   if (env_idle(P, state, eid)) return;
-  Sim<WaveHip, kN, kJ> s(P, state, g_smem, obs, eid, kRes);
+  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
   StepIn a;
   a.stage_idx = stage_idx[eid];
   a.num_exec = num_exec[eid];
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, con
   }
 }
 
-template <bool kRes, int kN, int kJ>
+template <bool kRes, int kN, int kJ, int kS>
 __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                 int kind, uint64_t seed, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, ui
   const int B = P->L.num_envs;
   const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   if (env_idle(P, state, eid) && action_log == nullptr && !autoreset) return;
-  Sim<WaveHip, kN, kJ> s(P, state, g_smem, obs, eid, kRes);
+  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
   s.load_hot();
   for (int k = 0; k < num_steps; ++k) {
 #ifdef SSIM_PROFILE
@@ -166,20 +166,24 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
   }
 }
 
-// Kernel variant for a layout: LDS-resident instantiations, specialised on (executors, jobs) for the
-// benchmark shape (BASELINE configs[1]: 10 executors, 50 jobs), else the generic ones.
+// Kernel variant for a layout: LDS-resident instantiations, fully specialised on (executors, jobs, stage cap)
+// for the benchmark shape (BASELINE configs[1]: 10 executors, 50 jobs, 50 x 18 stages of the TPC-H-format
+// dataset), else the generic ones.
 using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
 using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int, const double*, uint8_t*,
                           int32_t*, uint64_t*);
+static bool bench_shape(const Params& p) {
+  return p.L.num_executors == 10 && p.L.job_cap == 50 && p.L.stage_cap == 900;
+}
 static StepFn pick_step(const Params& p) {
-  if (!p.O.lds_resident) return k_step<false, 0, 0>;
-  if (p.L.num_executors == 10 && p.L.job_cap == 50) return k_step<true, 10, 50>;
-  return k_step<true, 0, 0>;
+  if (!p.O.lds_resident) return k_step<false, 0, 0, 0>;
+  if (bench_shape(p)) return k_step<true, 10, 50, 900>;
+  return k_step<true, 0, 0, 0>;
 }
 static RolloutFn pick_rollout(const Params& p) {
-  if (!p.O.lds_resident) return k_rollout<false, 0, 0>;
-  if (p.L.num_executors == 10 && p.L.job_cap == 50) return k_rollout<true, 10, 50>;
-  return k_rollout<true, 0, 0>;
+  if (!p.O.lds_resident) return k_rollout<false, 0, 0, 0>;
+  if (bench_shape(p)) return k_rollout<true, 10, 50, 900>;
+  return k_rollout<true, 0, 0, 0>;
 }
 
 // ------------------------------------------------------------------------------------------ C ABI
