@@ -55,7 +55,8 @@ __device__ __forceinline__ T ldg(const T* p, int64_t i) {
 
 // top-level phases (disjoint) then inclusive sub-timers (nested inside the top-level ones)
 enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kPhHandle, kPhPostScan, kPhObserve,
-                 kPhSample, kPhPool, kPhScan, kPhLoadSave, kPhPoolBig, kPhIdleOrder, kPhDraw,
+                 kPhSample, kPhPool, kPhScan, kPhLoadSave, kPhPoolBig, kPhIdleOrder, kPhDraw, kPhJobArr,
+                 kPhExecArr, kPhTaskDone, kPhStageDone,
                  // event counters (not cycles)
                  kCtPoolSmall, kCtPoolBig, kCtTask, kCtIdleOrder, kNumPhases };
 #ifdef SSIM_PROFILE
@@ -766,6 +767,7 @@ struct Sim {
   }
 
   __device__ __forceinline__ void trace(double t, int kind, int e, int job, int sid, int seq) {
+    if (L.trace_cap == 0) return;  // tracing off: no bookkeeping at all
     if (h.trace_len < L.trace_cap && W::lane() == 0) {
       TraceRec* r = reinterpret_cast<TraceRec*>(obs + L.ob_trace) + (int64_t)eid * L.trace_cap + h.trace_len;
       r->t = t;
@@ -1145,8 +1147,10 @@ struct Sim {
     }
     stage(g) = s;
     exr(e) = x;
+    SSIM_TIC(t_sd);
     bool changed = false;
     if (st_completed(g)) changed = stage_completed(j, g);
+    SSIM_TOC(t_sd, kPhStageDone);
     if (job_nact(j) == 0) job_completed(j);
     const bool had = release(e, g, changed);
     if (changed)
@@ -1221,15 +1225,23 @@ struct Sim {
       h.events++;
       h.step_events++;
       if (kind == kEvArrival) {
-        trace(t, kind, -1, g, -1, seq);
+        if (L.trace_cap > 0) trace(t, kind, -1, g, -1, seq);
+        SSIM_TIC(t_a);
         on_job_arrival(g);
+        SSIM_TOC(t_a, kPhJobArr);
       } else {
-        const int j = st_job(g);
-        trace(t, kind, e, j, g - job_base(j), seq);
-        if (kind == kEvReady)
+        if (L.trace_cap > 0) {
+          const int j = st_job(g);
+          trace(t, kind, e, j, g - job_base(j), seq);
+        }
+        SSIM_TIC(t_x);
+        if (kind == kEvReady) {
           on_executor_arrival(e, g);
-        else
+          SSIM_TOC(t_x, kPhExecArr);
+        } else {
           on_task_done(e, g);
+          SSIM_TOC(t_x, kPhTaskDone);
+        }
       }
       SSIM_TOC(t_h, kPhHandle);
       SSIM_TIC(t_s);

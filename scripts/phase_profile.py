@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.join(REPO, "gym-sparksched_amd"))
 
 PHASES = ["policy", "action", "round_check", "fulfill", "pop", "handle", "post_scan", "observe",
           "(sample)", "(pool ops)", "(scans)", "(hot load/save)", "(big-table staging)", "(idle_order)",
-          "(duration draw)", "#small-table ops", "#big-table ops", "#task launches", "#idle_order"]
+          "(duration draw)", "(job arrival)", "(executor arrival)", "(task done)", "(stage completion)",
+          "#small-table ops", "#big-table ops", "#task launches", "#idle_order"]
 TOP = 8  # the first TOP phases are disjoint; the rest are inclusive sub-timers
 
 
