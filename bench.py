@@ -4,8 +4,10 @@
 
 A "step" = one env.step for every env of the batch: device random policy reads the obs, then the step
 kernel applies the action, runs the discrete-event loop and writes the next observation to HBM.
-Modes: `rollout` (default: K steps of policy+step fused into one persistent launch) and `step`
-(two launches per step, the C-ABI call pattern of an external policy).
+Modes: `rollout` (default: K steps = K x envs decisions of policy+step fused into one launch, the decisions
+claimed from a shared budget so that envs with cheap decisions take more and the launch has no tail;
+`--lockstep` gives every env exactly K, and a lockstep launch is timed off the clock for comparison) and
+`step` (two launches per step, the C-ABI call pattern of an external policy).
 
 Output: one JSON line on rank 0. Multi-GPU: one process per GPU (torchrun), envs sharded per rank with
 no data-path collective (weak scaling); decisions are summed and time is max-reduced over ranks.
@@ -189,6 +191,9 @@ def main():
                     help="decima workload: run the PyTorch DecimaScheduler instead of the fused kernel")
     ap.add_argument("--ppo-time-limit", type=float, default=0.0,
                     help="ppo workload: override mean_time_limit (ms) of config/decima_tpch.yaml (0 = keep 2e7)")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="rollout mode: every env takes exactly `chunk` decisions per launch (ssim_rollout_ex) "
+                         "instead of sharing a budget of envs x chunk decisions (ssim_rollout_budget)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="rollout mode: leave finished envs idle instead of resetting them on the device")
     args = ap.parse_args()
@@ -245,7 +250,10 @@ def main():
             for k, c in enumerate(chunks(n)):
                 if events is not None:
                     events[2 * k].record(stream)
-                eng.rollout(kind, 1234, c, flags=flags, time_limits=limits)
+                if args.lockstep:
+                    eng.rollout(kind, 1234, c, flags=flags, time_limits=limits)
+                else:  # the same B x c decisions, claimed by whichever env is ready (no tail)
+                    eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=flags, time_limits=limits)
                 if events is not None:
                     events[2 * k + 1].record(stream)
         elif args.mode == "decima":
@@ -293,6 +301,19 @@ def main():
     t1 = time.perf_counter()
     counts1 = eng.views["counts"].cpu().numpy()
     acc1 = eng.views["acc"].cpu().numpy()
+    lockstep = None
+    if args.mode == "rollout" and not args.lockstep:
+        # off the clock: one lockstep launch of the same length (every env exactly `chunk` decisions) for
+        # comparison -- its time is set by the env whose `chunk` decisions cost the most
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        a0 = eng.views["acc"].cpu().numpy().copy()
+        ev[0].record(stream)
+        eng.rollout(kind, 1234, chunk, flags=flags, time_limits=limits)
+        ev[1].record(stream)
+        torch.cuda.synchronize(dev)
+        ld = float((eng.views["acc"].cpu().numpy() - a0).sum(axis=0)[_abi.ACC_DECISIONS])
+        lockstep = {"decisions": int(ld), "kernel_ms": ev[0].elapsed_time(ev[1]),
+                    "decisions_per_s": ld / (ev[0].elapsed_time(ev[1]) / 1e3)}
     errs = int(np.count_nonzero(counts1[:, _abi.OC_ERR] & _abi.SSIM_ERR_STICKY))
     d_acc = (acc1 - acc0).sum(axis=0).astype(np.float64)  # S_act, E_act, J_act, events, decisions, episodes
     decisions = int(d_acc[_abi.ACC_DECISIONS])  # over all episodes (auto-reset restarts the per-episode count)
@@ -338,6 +359,8 @@ def main():
                        "policy": ("torch" if args.torch_policy else "fused HIP kernel") if args.mode == "decima"
                        else "device random",
                        "steps_per_launch": chunk if args.mode == "rollout" else 1,
+                       "work_sharing": ("lockstep" if args.lockstep else "shared budget of envs x steps "
+                                        "decisions per launch") if args.mode == "rollout" else None,
                        "autoreset": bool(args.mode != "step" and (flags or args.mode == "decima")),
                        "parallelism": f"env-sharded x{world}"},
             "decisions": int(decisions),
@@ -353,6 +376,8 @@ def main():
                          "alg_bytes_per_launch": alg_bytes / world / launches},
             "cpu_baseline": None,
         }
+        if lockstep is not None:
+            line["lockstep_1gpu"] = lockstep
         if not args.no_cpu_baseline and world == 1 and args.workload == "tpch":
             procs = args.cpu_procs or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, procs)

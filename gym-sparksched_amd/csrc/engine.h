@@ -87,7 +87,9 @@ struct Params {
   uint8_t iv[kIvRows][4];
 };
 constexpr int64_t kParamsReserve = 4096;
-static_assert(sizeof(Params) <= kParamsReserve, "params block");
+// The last 64 B of the params block hold the shared-budget rollout's decision counter (ssim_rollout_budget).
+constexpr int64_t kTicketOffset = kParamsReserve - 64;
+static_assert(sizeof(Params) <= kTicketOffset, "params block");
 
 __host__ __device__ inline int exec_level_index(double key) {  // EXEC_LEVELS index, 0xFF if not a level
   return key == 5.0 ? 0 : key == 10.0 ? 1 : key == 20.0 ? 2 : key == 40.0 ? 3 : key == 50.0 ? 4

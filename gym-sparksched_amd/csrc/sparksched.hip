@@ -85,18 +85,37 @@ template <bool kRes, int kN, int kJ, int kS>
 __global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                 int kind, uint64_t seed, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
-                                                int32_t* action_log, uint64_t* prof_out) {
+                                                int32_t* action_log, uint64_t* prof_out, int64_t budget) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
   const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   if (env_idle(P, state, eid) && action_log == nullptr && !autoreset) return;
   Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
   s.load_hot();
+  // Shared budget (budget > 0): decisions are claimed from one device counter in chunks sized to what is
+  // left (guided self-scheduling: 8 early, 1 at the end), so the launch ends within ~one decision of the
+  // budget running out instead of waiting for the env with the most expensive K decisions.
+  unsigned long long* tickets =
+      budget > 0 ? reinterpret_cast<unsigned long long*>(state + kTicketOffset) : nullptr;
+  int64_t granted = 0, last = 0;
   for (int k = 0; k < num_steps; ++k) {
 #ifdef SSIM_PROFILE
     const uint64_t t0 = WaveHip::clock();
 #endif
     s.load_header();
+    if (tickets != nullptr) {
+      if (!autoreset && (s.h.terminated || s.frozen())) break;
+      if (granted == 0) {
+        int64_t c = (budget - last) / (4 * (int64_t)B);
+        c = c < 1 ? 1 : c > 8 ? 8 : c;
+        unsigned long long t = 0;
+        if (WaveHip::lane() == 0) t = atomicAdd(tickets, (unsigned long long)c);
+        last = (int64_t)WaveHip::uni((uint64_t)t);
+        if (last >= budget) break;
+        granted = budget - last < c ? budget - last : c;
+      }
+      --granted;
+    }
     const StepIn a = sim_policy(s, kind, seed);
 #ifdef SSIM_PROFILE
     s.prof[kPhPolicy] += WaveHip::clock() - t0;
@@ -171,7 +190,7 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
 // dataset), else the generic ones.
 using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
 using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int, const double*, uint8_t*,
-                          int32_t*, uint64_t*);
+                          int32_t*, uint64_t*, int64_t);
 static bool bench_shape(const Params& p) {
   return p.L.num_executors == 10 && p.L.job_cap == 50 && p.L.stage_cap == 900;
 }
@@ -300,19 +319,35 @@ extern "C" int ssim_policy(ssim_handle* h, int32_t kind, uint64_t seed, uint64_t
   return hip_check(hipGetLastError(), "k_policy launch");
 }
 
-extern "C" int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
-                               const double* time_limits, int32_t* action_log, void* stream) {
-  if (h == nullptr || num_steps < 0) return set_err(SSIM_E_ARG, "ssim_rollout: bad argument");
+static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int64_t budget,
+                          int32_t flags, const double* time_limits, int32_t* action_log, void* stream) {
+  if (h == nullptr || num_steps < 0 || budget < 0) return set_err(SSIM_E_ARG, "ssim_rollout: bad argument");
   if (kind != SSIM_POLICY_FAIR && kind != SSIM_POLICY_FIFO && kind != SSIM_POLICY_RANDOM)
     return set_err(SSIM_E_ARG, "ssim_rollout: unknown policy %d", kind);
   if ((flags & ~SSIM_ROLLOUT_AUTORESET) != 0) return set_err(SSIM_E_ARG, "ssim_rollout_ex: unknown flags 0x%x", flags);
   if ((flags & SSIM_ROLLOUT_AUTORESET) && !(h->params.C.job_arrival_gap > 0.0))
     return set_err(SSIM_E_ARG, "ssim_rollout_ex: auto-reset needs job_arrival_gap in the config");
   const ssim_layout& L = h->params.L;
+  if (budget > 0) {
+    if (hip_check(hipMemsetAsync(h->state + kTicketOffset, 0, 8, (hipStream_t)stream), "ticket reset") != SSIM_OK)
+      return SSIM_E_HIP;
+  }
   hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, flags, time_limits, h->reset, action_log,
-                     (uint64_t*)nullptr);
+                     (uint64_t*)nullptr, budget);
   return hip_check(hipGetLastError(), "k_rollout launch");
+}
+
+extern "C" int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
+                               const double* time_limits, int32_t* action_log, void* stream) {
+  return rollout_launch(h, kind, seed, num_steps, 0, flags, time_limits, action_log, stream);
+}
+
+extern "C" int ssim_rollout_budget(ssim_handle* h, int32_t kind, uint64_t seed, int32_t max_steps,
+                                   int64_t total_decisions, int32_t flags, const double* time_limits,
+                                   int32_t* action_log, void* stream) {
+  if (total_decisions <= 0) return set_err(SSIM_E_ARG, "ssim_rollout_budget: total_decisions must be > 0");
+  return rollout_launch(h, kind, seed, max_steps, total_decisions, flags, time_limits, action_log, stream);
 }
 
 extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t* action_log,
@@ -338,7 +373,7 @@ extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed
   const ssim_layout& L = h->params.L;
   hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, 0, (const double*)nullptr, h->reset,
-                     (int32_t*)nullptr, prof_out);
+                     (int32_t*)nullptr, prof_out, (int64_t)0);
   return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
 }
 #endif

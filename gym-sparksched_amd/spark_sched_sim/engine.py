@@ -289,6 +289,20 @@ class DeviceEngine:
             self.handle, kind, seed, num_steps, flags, None if tl is None else tl.data_ptr(), ptr, self._stream()),
             "ssim_rollout")
 
+    def rollout_budget(self, kind: int, seed: int, max_steps: int, total_decisions: int, action_log=None,
+                       flags: int = 0, time_limits=None):
+        """Work-conserving rollout (ssim_rollout_budget): `total_decisions` decisions shared by all envs, each
+        env at most `max_steps`; each env's decisions equal those of `rollout`, only their number differs."""
+        ptr = action_log.data_ptr() if action_log is not None else None
+        tl = None
+        if time_limits is not None:
+            tl = self.torch.as_tensor(np.asarray(time_limits, dtype=np.float64).reshape(self.num_envs),
+                                      device=self.device) if not hasattr(time_limits, "data_ptr") else time_limits
+        self._keep_tl = tl
+        self._native.check(self._native.lib().ssim_rollout_budget(
+            self.handle, kind, seed, max_steps, total_decisions, flags, None if tl is None else tl.data_ptr(), ptr,
+            self._stream()), "ssim_rollout_budget")
+
     def host_views(self) -> dict:
         return arena_views(self.obs.cpu().numpy(), self.layout)
 

@@ -187,6 +187,17 @@ int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
 int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
                     const double* time_limits, int32_t* action_log, void* stream);
 
+/* Work-conserving rollout: a shared budget of `total_decisions` decisions over all envs (each env at most
+ * `max_steps`), claimed from a device counter in chunks sized to what is left. Envs whose decisions are cheap
+ * take more of the budget, so the launch ends when the budget is spent rather than when the env with the most
+ * expensive `num_steps` decisions finishes (cf. the reference's fixed-duration RolloutWorkerAsync,
+ * trainers/rollout_worker.py:160-206, which stops each worker by wall time rather than by step count).
+ * Each env's decisions are the same as in ssim_rollout_ex (its policy counter is its own decision count);
+ * only how many each env takes differs. action_log rows [max_steps][num_envs][2]; rows an env did not reach
+ * are left untouched. Terminated envs stop claiming unless SSIM_ROLLOUT_AUTORESET is set. */
+int ssim_rollout_budget(ssim_handle* h, int32_t kind, uint64_t seed, int32_t max_steps, int64_t total_decisions,
+                        int32_t flags, const double* time_limits, int32_t* action_log, void* stream);
+
 /* Per-job results for metrics (spark_sched_sim/metrics.py): t_arrival/t_completed float64 [num_envs][job_cap]
  * and job state int32 [num_envs][job_cap] (0 not arrived, 1 active, 2 completed), any may be NULL. */
 int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32_t* state, void* stream);

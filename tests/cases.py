@@ -72,16 +72,25 @@ def case_lockstep_config(make, dataset, env_cfg, cfg_over, B, seed0, pol):
     parity.compare_job_times(ta, tc, oracles)
 
 
-def case_rollout_replay(make, dataset, env_cfg, kind, B=64, K=400, stride=4):
+def case_rollout_replay(make, dataset, env_cfg, kind, B=64, K=400, stride=4, budget=0):
     """ssim_rollout (policy+step fused in one launch) logs its actions; replaying them on the oracle
-    reproduces the trace, job times, decision counts and final observation bit-exactly."""
+    reproduces the trace, job times, decision counts and final observation bit-exactly. budget > 0: the
+    work-conserving ssim_rollout_budget (B*budget decisions shared by the envs, at most K each)."""
     eng = make(env_cfg, B, dataset, 8000)
     seeds = [5000 + i for i in range(B)]
     eng.reset(seeds=seeds)
     log = eng.alloc_action_log(K)
-    eng.rollout(kind, 99, K, log)
+    if budget:
+        eng.rollout_budget(kind, 99, K, B * budget, log)
+    else:
+        eng.rollout(kind, 99, K, log)
     log = np.asarray(eng.to_numpy(log))
     v = eng.host_views()
+    if budget:
+        dec = v["counts"][:, _abi.OC_DECISIONS].astype(np.int64)
+        live = (v["counts"][:, _abi.OC_TERMINATED] == 0) & (dec < K)
+        assert dec.sum() <= B * budget and (dec.sum() == B * budget or not live.any())
+        assert dec.max() > dec.min()  # the budget went unevenly (cheap envs took more)
     ta, tc, _ = eng.job_times_np()
     for i in range(0, B, stride):
         o = SparkSchedOracle(env_cfg, dataset)

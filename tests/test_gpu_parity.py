@@ -43,6 +43,11 @@ def test_rollout_replay(make, dataset, env_cfg, kind):
     cases.case_rollout_replay(make, dataset, env_cfg, kind)
 
 
+@pytest.mark.parametrize("kind", [_abi.SSIM_POLICY_RANDOM, _abi.SSIM_POLICY_FAIR])
+def test_rollout_budget_replay(make, dataset, env_cfg, kind):
+    cases.case_rollout_replay(make, dataset, env_cfg, kind, B=64, K=400, stride=4, budget=150)
+
+
 def test_rollout_replay_full_episodes(make, dataset, env_cfg):
     cases.case_rollout_replay(make, dataset, env_cfg, _abi.SSIM_POLICY_RANDOM, B=256, K=2500, stride=32)
 
