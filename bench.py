@@ -6,7 +6,8 @@ A "step" = one env.step for every env of the batch: device random policy reads t
 kernel applies the action, runs the discrete-event loop and writes the next observation to HBM.
 Modes: `rollout` (default: K steps = K x envs decisions of policy+step fused into one launch, the decisions
 claimed from a shared budget so that envs with cheap decisions take more and the launch has no tail;
-`--lockstep` gives every env exactly K, and a lockstep launch is timed off the clock for comparison) and
+`--lockstep` gives every env exactly K; `--compare-lockstep` times one lockstep launch off the clock beside
+the budget launch) and
 `step` (two launches per step, the C-ABI call pattern of an external policy).
 
 Output: one JSON line on rank 0. Multi-GPU: one process per GPU (torchrun), envs sharded per rank with
@@ -194,6 +195,9 @@ def main():
     ap.add_argument("--lockstep", action="store_true",
                     help="rollout mode: every env takes exactly `chunk` decisions per launch (ssim_rollout_ex) "
                          "instead of sharing a budget of envs x chunk decisions (ssim_rollout_budget)")
+    ap.add_argument("--compare-lockstep", action="store_true",
+                    help="rollout mode: after the timed region, time one lockstep launch of the same length "
+                         "(off by default so a rocprof of the default run sees only warm-up + timed launches)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="rollout mode: leave finished envs idle instead of resetting them on the device")
     args = ap.parse_args()
@@ -302,7 +306,7 @@ def main():
     counts1 = eng.views["counts"].cpu().numpy()
     acc1 = eng.views["acc"].cpu().numpy()
     lockstep = None
-    if args.mode == "rollout" and not args.lockstep:
+    if args.mode == "rollout" and not args.lockstep and args.compare_lockstep:
         # off the clock: one lockstep launch of the same length (every env exactly `chunk` decisions) for
         # comparison -- its time is set by the env whose `chunk` decisions cost the most
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
