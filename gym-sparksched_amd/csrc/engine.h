@@ -65,7 +65,9 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
 #define SSIM_COUNT(ph) (void)0
 #endif
 enum : int32_t { kPoolNone = -1, kPoolCommon = 0 };
-enum : int32_t { kEvArrival = 1, kEvTask = 2, kEvReady = 3, kTrJobDone = 4 };
+// trace-only kinds: a job completion (:682-697) and an executor released to the common pool (:779-782, the
+// reference's Executor.add_history(wall, -1)); with the kEvReady records they give the render history.
+enum : int32_t { kEvArrival = 1, kEvTask = 2, kEvReady = 3, kTrJobDone = 4, kTrToCommon = 5 };
 enum : int32_t { kJobPending = 0, kJobActive = 1, kJobDone = 2 };
 enum : int32_t { kScanAll = 0, kScanOnly = 1, kScanExcept = 2 };
 
@@ -983,7 +985,10 @@ struct Sim {
     for (int k = 0; k < n; ++k) {
       const int e = ld(ids + k);
       move_to_pool(e, dst, false);
-      if (dst == kPoolCommon) detach(j, e);
+      if (dst == kPoolCommon) {
+        detach(j, e);
+        if (L.trace_cap > 0) trace(h.wall, kTrToCommon, e, j, -1, -1);
+      }
     }
   }
   __device__ __forceinline__ void release_idle_one(int src, int e) {

@@ -28,6 +28,8 @@ OC_NUM_ARRIVED, OC_TRACE_LEN, OC_STEP_EVENTS, OC_EPISODE = range(12, 16)
 NUM_COUNTS = 16
 RESET_HEAD_BYTES = 64
 TRACE_BYTES = 32
+# trace record kinds: events (arrival, task finished, executor ready) and trace-only records
+TR_ARRIVAL, TR_TASK, TR_READY, TR_JOB_DONE, TR_TO_COMMON = range(1, 6)
 
 
 class SsimConfig(ct.Structure):

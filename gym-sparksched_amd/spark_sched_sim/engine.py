@@ -82,6 +82,25 @@ def decode_trace(raw_u8: np.ndarray, n: int):
             for i in range(n)]
 
 
+def executor_histories(records, num_executors: int) -> list[list[list]]:
+    """Executor.history (executor.py:22-44) rebuilt from one episode's trace records: an EXECUTOR_READY
+    event attaches the executor to its job (spark_sched_sim.py:445), a TO_COMMON record releases it to the
+    common pool (:782). Each history is [[t_release, job_id], ...] starting from [None, -1], the last entry
+    open (t = None) -- the renderer's input (spark_sched_sim.py:411, renderer.py:84-95)."""
+    hist = [[[None, -1]] for _ in range(num_executors)]
+    for t, kind, e, j, _s, _q in records:
+        if kind == _abi.TR_READY:
+            job = j
+        elif kind == _abi.TR_TO_COMMON:
+            job = -1
+        else:
+            continue
+        h = hist[e]
+        h[-1][0] = t
+        h.append([None, job])
+    return hist
+
+
 def obs_dict(v: dict, env: int) -> dict:
     """Reference-format observation of one env (spark_sched_sim.py:393-399) from host (numpy) views."""
     from collections import namedtuple

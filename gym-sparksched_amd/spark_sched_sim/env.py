@@ -16,7 +16,7 @@ from typing import Any
 import numpy as np
 
 from . import _abi
-from .engine import DeviceEngine, obs_dict
+from .engine import DeviceEngine, decode_trace, executor_histories, obs_dict
 from .spaces import ActionSpace
 
 NUM_NODE_FEATURES = 3
@@ -43,7 +43,7 @@ class SparkSchedSimEnv:
     metadata = {"render_modes": ["human"], "render_fps": 30}
 
     def __init__(self, env_cfg: dict[str, Any], dataset=None, device="cuda", job_cap: int | None = None,
-                 _engine_factory=None):
+                 history_cap: int = 0, _engine_factory=None):
         self.num_executors: int = env_cfg["num_executors"]
         self.moving_delay = env_cfg["moving_delay"]
         self.beta = env_cfg.get("beta", 0)
@@ -58,7 +58,10 @@ class SparkSchedSimEnv:
             from .data_samplers.synthetic_tpch import generate
 
             dataset = generate(0)
-        factory = _engine_factory or (lambda cfg, ds: DeviceEngine(cfg, 1, ds, device=device, job_cap=job_cap))
+        # history_cap > 0 records the per-episode event trace (that many records) for render_data()
+        self.history_cap = int(history_cap)
+        factory = _engine_factory or (lambda cfg, ds: DeviceEngine(cfg, 1, ds, device=device, job_cap=job_cap,
+                                                                   trace_cap=self.history_cap))
         self._eng = factory(dict(env_cfg), dataset)
         self.action_space = ActionSpace(self.num_executors)
         self.job_duration_buff: deque = deque(maxlen=200)
@@ -126,6 +129,41 @@ class SparkSchedSimEnv:
         n = int(self._counts()[_abi.OC_NUM_ARRIVED]) if self._have_episode else 0
         total = self.job_arrival_cap or 0
         return ta[0][:total], tc[0][:total], st[0][:total], n
+
+    # -- render data (spark_sched_sim.py:408-426 `_render_frame`; drawing itself needs pygame) ---------
+    def _trace(self) -> list:
+        if self.history_cap <= 0:
+            raise ValueError("render data needs SparkSchedSimEnv(..., history_cap=N)")
+        v = self._eng.host_views()
+        n = int(v["counts"][0][_abi.OC_TRACE_LEN])
+        if n > self.history_cap:
+            raise RuntimeError(f"event trace overflowed history_cap={self.history_cap} ({n} records)")
+        return decode_trace(np.asarray(v["trace"][0]), n)
+
+    def executor_histories(self) -> list[list[list]]:
+        """Executor.history of every executor for the current episode (executor.py:22-44)."""
+        return executor_histories(self._trace(), self.num_executors)
+
+    def render_data(self) -> dict:
+        """The arguments `_render_frame` (spark_sched_sim.py:408-424) hands to the renderer: executor
+        histories, completion times of the completed jobs (in the reference's set order), wall time, average job
+        duration (int seconds, metrics.avg_job_duration * 1e-3), active and completed job counts."""
+        from . import metrics
+
+        recs = self._trace()
+        # the reference iterates its `completed_job_ids` set: a set built by the same add() sequence (completion
+        # order, no removals within an episode) iterates in the same order
+        t_done, completed = {}, set()
+        for t, kind, _e, j, _s, _q in recs:
+            if kind == _abi.TR_JOB_DONE:
+                t_done[j] = t
+                completed.add(j)
+        return {"executor_histories": executor_histories(recs, self.num_executors),
+                "job_completion_times": [t_done[j] for j in completed],
+                "wall_time": self.wall_time,
+                "average_job_duration": int(metrics.avg_job_duration(self) * 1e-3),
+                "num_active_jobs": self.num_active_jobs,
+                "num_jobs_completed": self.num_completed_jobs}
 
     # -- internals ----------------------------------------------------------------------------------
     def _counts(self):

@@ -27,7 +27,7 @@ import torch
 from .. import _abi
 from ..schedulers.decima import DecimaScheduler, select_envs
 from .returns import Baseline, ReturnsCalculator
-from .rollouts import RolloutCollector
+from .rollouts import AsyncRolloutCollector, RolloutCollector
 
 EPS = 1e-8  # ppo.py:13
 
@@ -88,7 +88,16 @@ class PPO:
             def engine_factory(cfg, n, ds):
                 return DeviceEngine(cfg, n, ds, device=self.device)
         self.engine = engine_factory({k: v for k, v in env_cfg.items() if k != "mean_time_limit"}, B, dataset)
-        self.collector = RolloutCollector(self.engine, self.scheduler, seed=self.seed * 7919 + self.rank)
+        self.rollout_duration = train_cfg.get("rollout_duration")  # trainer.py:63, async workers :277-279
+        if self.rollout_duration:
+            S_tot = self.num_sequences * self.world
+            base = [self.seed + self.rank * self.num_sequences + s for s in range(self.num_sequences)
+                    for _ in range(self.num_rollouts)]
+            self.collector = AsyncRolloutCollector(self.engine, self.scheduler, self.rollout_duration, base, S_tot,
+                                                   mean_time_limit=self.mean_time_limit,
+                                                   seed=self.seed * 7919 + self.rank)
+        else:
+            self.collector = RolloutCollector(self.engine, self.scheduler, seed=self.seed * 7919 + self.rank)
         self.gen = torch.Generator(device=self.device).manual_seed(self.seed * 7919 + self.rank)
         self.time_limit_rngs = None
         if self.mean_time_limit:
@@ -118,8 +127,10 @@ class PPO:
         return np.array(lim)
 
     def collect(self):
-        seeds = self._seeds()
         self.scheduler.eval()
+        if self.rollout_duration:
+            return self.collector.collect(generator=self.gen)
+        seeds = self._seeds()
         buf = self.collector.collect(seeds, self._time_limits(seeds), generator=self.gen)
         self.reset_count += 1
         return buf

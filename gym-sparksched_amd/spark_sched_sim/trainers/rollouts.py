@@ -10,9 +10,11 @@ The reference runs one env per process (RolloutWorkerSync); here a "worker" is a
 
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .. import _abi
+from ..wrappers import StochasticTimeLimitSampler
 from ..schedulers.decima import DagBatch, build_batch, cat_batches, select_envs
 
 
@@ -28,6 +30,7 @@ class GpuRolloutBuffer:
         self.job_idx: list[torch.Tensor] = []
         self.exec_idx: list[torch.Tensor] = []
         self.lgprobs: list[torch.Tensor] = []
+        self.num_exec: list[torch.Tensor] = []  # the action the env applied (DecimaActWrapper: 1 + exec_idx)
         self.rewards: list[torch.Tensor] = []
         self.wall_before: list[torch.Tensor] = []
         self.final_wall: torch.Tensor | None = None
@@ -39,6 +42,7 @@ class GpuRolloutBuffer:
         self.job_idx.append(act["job_idx"][envs])
         self.exec_idx.append(act["exec_idx"][envs])
         self.lgprobs.append(act["lgprob"][envs])
+        self.num_exec.append(act["num_exec"][envs])
         self.rewards.append(reward)
         self.wall_before.append(wall_before)
 
@@ -103,8 +107,39 @@ class RolloutCollector:
         f = {k: torch.from_numpy(x).to(dev) for k, x in eng.decima_features_np(*self.scales).items()}
         return v, f
 
+    def _decide_and_step(self, alive: torch.Tensor, generator=None):
+        """One batched decision for the `alive` envs (the others get an invalid action and stay untouched),
+        then one engine step. Returns (live env ids, their observations as a DagBatch, action dict, views)."""
+        eng = self.engine
+        v, f = self._views()
+        b_all = build_batch(v, f, env_mask=alive)
+        if self.on_device and self.fused:  # one fused kernel launch (ssim_decima_policy)
+            self.counter += 1
+            fo = self.policy.schedule_fused(eng, f, seed=self.seed, counter=self.counter, env_mask=alive,
+                                            node_cap=int(b_all.num_nodes.max().item()))
+            act = {"stage_idx": fo["stage_idx"], "num_exec": fo["num_exec"], "job_idx": fo["job_idx"].long(),
+                   "exec_idx": fo["exec_idx"].long(), "lgprob": fo["lgprob"]}
+        else:
+            act = self.policy.schedule(b_all, generator=generator)
+        envs = torch.nonzero(alive).squeeze(1)
+        batch = select_envs(b_all, envs)
+        si = torch.where(alive, act["stage_idx"], torch.full_like(act["stage_idx"], -2))
+        if self.on_device:
+            eng.step(si, act["num_exec"])
+        else:
+            eng.step(si.cpu().numpy(), act["num_exec"].cpu().numpy())
+        v, _ = self._views(features=False)
+        return envs, batch, act, v
+
+    @staticmethod
+    def _done(v) -> torch.Tensor:
+        c = v["counts"]
+        return (c[:, _abi.OC_TERMINATED] != 0) | (c[:, _abi.OC_TRUNCATED] != 0)
+
     @torch.no_grad()
     def collect(self, seeds, time_limits=None, generator=None, max_steps: int = 10**9) -> GpuRolloutBuffer:
+        """RolloutWorkerSync.collect_rollout (rollout_worker.py:135-157): reset every env with its seed,
+        step until each env's episode ends."""
         eng = self.engine
         B = eng.num_envs
         limits = None if time_limits is None else torch.as_tensor(time_limits, dtype=torch.float64)
@@ -118,29 +153,78 @@ class RolloutCollector:
         for _ in range(max_steps):
             if not bool(alive.any()):
                 break
-            v, f = self._views()
-            b_all = build_batch(v, f, env_mask=alive)
-            if self.on_device and self.fused:  # one fused kernel launch (ssim_decima_policy)
-                self.counter += 1
-                fo = self.policy.schedule_fused(eng, f, seed=self.seed, counter=self.counter, env_mask=alive,
-                                                node_cap=int(b_all.num_nodes.max().item()))
-                act = {"stage_idx": fo["stage_idx"], "num_exec": fo["num_exec"], "job_idx": fo["job_idx"].long(),
-                       "exec_idx": fo["exec_idx"].long(), "lgprob": fo["lgprob"]}
-            else:
-                act = self.policy.schedule(b_all, generator=generator)
-            envs = torch.nonzero(alive).squeeze(1)
-            batch = select_envs(b_all, envs)
-            si = torch.where(alive, act["stage_idx"], torch.full_like(act["stage_idx"], -2))
-            if self.on_device:
-                eng.step(si, act["num_exec"])
-            else:
-                eng.step(si.cpu().numpy(), act["num_exec"].cpu().numpy())
-            v, _ = self._views(features=False)
-            c = v["counts"]
+            envs, batch, act, v = self._decide_and_step(alive, generator)
             reward = v["reward"][envs].double()
             buf.add(batch, envs, act, reward, wall[envs])
             wall = torch.where(alive, v["wall_time"].double(), wall)
-            done = (c[:, _abi.OC_TERMINATED] != 0) | (c[:, _abi.OC_TRUNCATED] != 0)
-            alive = alive & ~done
+            alive = alive & ~self._done(v)
         buf.final_wall = wall
+        return buf
+
+
+class AsyncRolloutCollector(RolloutCollector):
+    """RolloutWorkerAsync (rollout_worker.py:160-206): model updates at regular intervals of simulated time,
+    regardless of episode boundaries. Each env (a "worker" row) keeps its episode across `collect` calls and
+    steps until `rollout_duration` ms of simulated time have elapsed in this call; an env whose episode ends
+    is reset in place with seed = base_seed + seed_step * reset_count (rollout_worker.py:118-120) and a new
+    StochasticTimeLimit draw. Times stored in the buffer are the elapsed time of the call (the reference's
+    `elapsed_time`), so the buffer feeds the same returns/baseline code as the sync collector; `buf.resets`
+    holds (env, step) pairs like RolloutBuffer.add_reset (the reference's returns ignore them too)."""
+
+    def __init__(self, engine, policy, rollout_duration: float, base_seeds, seed_step: int,
+                 mean_time_limit: float | None = None, **kw):
+        super().__init__(engine, policy, **kw)
+        B = engine.num_envs
+        self.rollout_duration = float(rollout_duration)
+        self.base_seeds = np.asarray(base_seeds, dtype=np.int64).reshape(B)
+        self.seed_step = int(seed_step)
+        self.reset_count = np.zeros(B, dtype=np.int64)
+        self.limits = None if not mean_time_limit else StochasticTimeLimitSampler(mean_time_limit, B)
+        self.next_wall = None  # wall time before each env's next decision (0 after a reset)
+
+    def _reset(self, env_ids: np.ndarray) -> None:
+        B = self.engine.num_envs
+        mode = np.zeros(B, dtype=np.uint8)
+        seeds = np.zeros(B, dtype=np.uint64)
+        lim = np.full(B, np.inf)
+        mode[env_ids] = _abi.SSIM_RESET_SEED
+        for e in env_ids:
+            seeds[e] = int(self.base_seeds[e] + self.seed_step * self.reset_count[e])
+            if self.limits is not None:
+                lim[e] = self.limits.sample(int(e), int(seeds[e]))
+        self.reset_count[env_ids] += 1
+        self.engine.reset_sampled(mode, seeds=seeds, time_limits=None if self.limits is None else lim)
+
+    @torch.no_grad()
+    def collect(self, generator=None, max_steps: int = 10**9) -> GpuRolloutBuffer:
+        B = self.engine.num_envs
+        if self.next_wall is None:  # first call: reset every worker (rollout_worker.py:174-176)
+            self._reset(np.arange(B))
+        v, _ = self._views(features=False)
+        dev = v["counts"].device
+        if self.next_wall is None:
+            self.next_wall = torch.zeros(B, dtype=torch.float64, device=dev)
+        buf = GpuRolloutBuffer(B)
+        buf.resets = []
+        elapsed = torch.zeros(B, dtype=torch.float64, device=dev)
+        step = torch.zeros(B, dtype=torch.long, device=dev)
+        alive = elapsed < self.rollout_duration
+        for _ in range(max_steps):
+            if not bool(alive.any()):
+                break
+            envs, batch, act, v = self._decide_and_step(alive, generator)
+            reward = v["reward"][envs].double()
+            buf.add(batch, envs, act, reward, elapsed[envs])
+            new_wall = v["wall_time"].double()
+            elapsed = torch.where(alive, elapsed + (new_wall - self.next_wall), elapsed)
+            self.next_wall = torch.where(alive, new_wall, self.next_wall)
+            done = alive & self._done(v)
+            if bool(done.any()):
+                ids = torch.nonzero(done).squeeze(1)
+                buf.resets += [(int(e), int(k)) for e, k in zip(ids.tolist(), step[ids].tolist())]
+                self._reset(ids.cpu().numpy())
+                self.next_wall[ids] = 0.0
+            step += alive.long()
+            alive = alive & (elapsed < self.rollout_duration)
+        buf.final_wall = elapsed
         return buf

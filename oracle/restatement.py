@@ -18,8 +18,9 @@ RNG consumption are reference-faithful by construction; those boundaries are pin
 ``tests/test_oracle_kats.py``. End-to-end parity against the reference itself is **unpinned** (no reference
 run and no reference fixtures exist); the committed fixtures in ``tests/golden/`` are produced by this module.
 
-Only behaviour on the hot path is restated; rendering/history (``renderer.py``, ``Executor.history``) is out
-of scope and omitted.
+Only behaviour on the hot path is restated; drawing (``renderer.py``, pygame) is out of scope, but the data
+the renderer draws — ``Executor.history`` (executor.py:22-44, appended at spark_sched_sim.py:445,782) — is
+kept, as the checker of the device's render-history export.
 """
 
 from __future__ import annotations
@@ -39,6 +40,7 @@ EXEC_LEVELS = [5, 10, 20, 40, 50, 60, 80, 100]  # tpch.py:238
 COMMON = (None, None)  # executor_tracker.py:10 COMMON_POOL_KEY
 ARRIVAL, TASK_DONE, EXEC_READY = 1, 2, 3  # event.py:9-12 (auto() order)
 JOB_DONE = 4  # trace-only record kind (job completion, spark_sched_sim.py:682-697)
+TO_COMMON = 5  # trace-only record kind (executor released to the common pool, spark_sched_sim.py:779-782)
 
 GraphInstance = namedtuple("GraphInstance", ["nodes", "edges", "edge_links"])  # gymnasium.spaces.GraphInstance
 
@@ -141,10 +143,16 @@ class _Job:
 
 
 class _Executor:
-    __slots__ = ("eid", "task_stage", "job", "executing")
+    __slots__ = ("eid", "task_stage", "job", "executing", "history")
 
     def __init__(self, eid):  # executor.py:5-27
         self.eid, self.task_stage, self.job, self.executing = eid, None, None, False
+        self.history = [[None, -1]]  # render-only (executor.py:22-25)
+
+    def add_history(self, wall_time, job_id):  # executor.py:34-44
+        if len(self.history) > 0:
+            self.history[-1][0] = wall_time
+        self.history += [[None, job_id]]
 
 
 class InvariantError(AssertionError):
@@ -476,6 +484,7 @@ class SparkSchedOracle:
         _check(ex.task_stage is None, "[attach_executor]")
         job.local.add(e)
         ex.job = job.jid
+        ex.add_history(self.wall_time, job.jid)  # :445
         self.moving_to[st.key] -= 1
         _check(self.moving_to[st.key] >= 0, "[record_executor_arrival]")
         self._move_to_pool(e, (job.jid, None))
@@ -632,6 +641,8 @@ class SparkSchedOracle:
             self._move_to_pool(e, dst)
             if dst == COMMON:
                 self._detach_from(self.jobs[jid], self.executors[e])
+                self.executors[e].add_history(self.wall_time, -1)  # :782
+                self._log(TO_COMMON, e, jid, -1, -1)
 
     def _detach_from(self, job, ex):  # job.py:84-89 via spark_sched_sim.py:779-782
         job.local.remove(ex.eid)

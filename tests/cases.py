@@ -471,3 +471,71 @@ def case_decima_fused(make, dataset, env_cfg, cfg_over, B, seed0, iters=12, devi
         assert int(np.count_nonzero(np.asarray(c)[:, _abi.OC_ERR])) == 0
         eng.rollout(_abi.SSIM_POLICY_RANDOM, 3 + it, 4)
     assert checked > B * iters // 2
+
+
+def case_async_rollouts(make, dataset, env_cfg, device="cpu", B=6, calls=3, duration=2.5e5, mean_limit=4e5):
+    """AsyncRolloutCollector (trainers/rollout_worker.py:160-206, RolloutWorkerAsync): episodes span
+    `collect` calls, each call runs every env for `duration` ms of simulated time, finished episodes are reset
+    in place with seed = base + seed_step * reset_count and a fresh StochasticTimeLimit draw. The applied
+    actions are replayed on the oracle through the reference's async loop (restated below); per env and call
+    the decision count, the elapsed times (bit-exact), rewards (1e-9 rel), reset steps and the final
+    observation must agree."""
+    import torch
+
+    from spark_sched_sim.schedulers.decima import DecimaScheduler
+    from spark_sched_sim.trainers import AsyncRolloutCollector
+
+    cfg = dict(env_cfg, num_executors=4, job_arrival_cap=6, job_arrival_rate=1e-4)
+    eng = make(cfg, B, dataset, 0)
+    torch.manual_seed(3)
+    pol = DecimaScheduler(4).to(device)  # decima_tpch.yaml architecture: the fused kernel on the device
+    base = [11 + i // 2 for i in range(B)]  # trainer.py:265-267: num_rollouts=2 rows per sequence
+    col = AsyncRolloutCollector(eng, pol, duration, base, 3, mean_time_limit=mean_limit, fused=True, seed=5)
+    gen = torch.Generator(device=device).manual_seed(1)
+    bufs = [col.collect(generator=gen) for _ in range(calls)]
+    v = eng.host_views()
+    total_resets = 0
+    for e in range(B):
+        o = SparkSchedOracle(cfg, dataset)
+        rng, reset_count = np.random.RandomState(42), 0
+        limit = None
+
+        def reset():
+            nonlocal rng, reset_count, limit
+            seed = base[e] + 3 * reset_count
+            if seed:  # stochastic_time_limit.py:15-16
+                rng = np.random.RandomState(seed)
+            limit = float(rng.exponential(mean_limit))
+            ob, _ = o.reset(seed=seed, options={"time_limit": limit})
+            reset_count += 1
+            return ob
+
+        ob = reset()
+        next_wall = 0.0
+        for c, buf in enumerate(bufs):
+            times, rewards, lengths, sample = buf.trajectories()
+            flat_si = torch.cat(buf.stage_idx).cpu().numpy()
+            flat_ne = torch.cat(buf.num_exec).cpu().numpy()
+            n = int(lengths[e])
+            elapsed, k, resets = 0.0, 0, []
+            while elapsed < duration:
+                wall = next_wall
+                assert k < n, f"env{e} call{c}: device stopped after {n} decisions, oracle continues"
+                i = int(sample[e, k])
+                ob, rew, term, trunc, info = o.step({"stage_idx": int(flat_si[i]), "num_exec": int(flat_ne[i])})
+                trunc = trunc or info["wall_time"] >= limit
+                assert float(times[e, k]) == elapsed, f"env{e} call{c} step{k} elapsed"
+                assert parity.close_rel(float(rewards[e, k]), rew), f"env{e} call{c} step{k} reward"
+                next_wall = info["wall_time"]
+                elapsed += next_wall - wall
+                if term or trunc:
+                    ob = reset()
+                    next_wall = 0.0
+                    resets.append(k)
+                k += 1
+            assert k == n, f"env{e} call{c}: {n} device decisions, oracle {k}"
+            assert float(times[e, n]) == elapsed
+            assert sorted(kk for ee, kk in buf.resets if ee == e) == resets
+            total_resets += len(resets)
+        parity.compare_obs(ob, obs_dict(v, e), f"env{e} final")
+    assert total_resets >= B, total_resets

@@ -135,3 +135,37 @@ def test_decima_env_wrapper_matches_reference_wrapper(dataset, env_cfg):
         parity.compare_decima(decima_observation(robs, N), obs, f"step {steps}")
         steps += 1
     assert steps > 100
+
+
+def test_render_history_matches_oracle(dataset, env_cfg):
+    """Render data export (spark_sched_sim.py:408-424): executor histories (executor.py:22-44) rebuilt from the
+    engine's event trace equal the oracle's Executor.history lists, mid-episode and at the end; completion
+    times follow the reference's completed-job set order."""
+    from hostsim.driver import HostEngine
+
+    cap = 1 << 16
+    env = SparkSchedSimEnv(env_cfg, dataset, history_cap=cap,
+                           _engine_factory=lambda cfg, ds: HostEngine(cfg, 1, ds, trace_cap=cap))
+    check_render_history(env, R.SparkSchedOracle(env_cfg, dataset))
+
+
+def check_render_history(env, ref):
+    pol = RandomPolicy(seed=4)
+    obs, _ = env.reset(seed=77)
+    robs, _ = ref.reset(seed=77)
+    done, steps, moves = False, 0, 0
+    while not done:
+        a, _ = pol.schedule(robs)
+        obs, _, done, _, _ = env.step(a)
+        robs, _, _, _, _ = ref.step(a)
+        steps += 1
+        if steps % 40 == 0 or done:
+            got = env.executor_histories()
+            want = [ex.history for ex in ref.executors]
+            assert got == want, f"step {steps}"
+    moves = sum(len(h) - 1 for h in got)
+    assert moves > 20 and any(j == -1 for h in got for _, j in h[1:])  # attachments and releases to COMMON
+    rd = env.render_data()
+    assert rd["job_completion_times"] == [ref.jobs[j].t_completed for j in ref.completed_ids]
+    assert rd["average_job_duration"] == int(R.avg_job_duration(ref) * 1e-3)
+    assert rd["num_jobs_completed"] == len(ref.completed_ids) and rd["wall_time"] == ref.wall_time

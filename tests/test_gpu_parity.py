@@ -73,3 +73,17 @@ def test_sampled_reset(make, dataset, env_cfg, cfg_over, B, seed0, mean_limit):
 @pytest.mark.parametrize("mean_limit", [None, 2.0e5])
 def test_autoreset_replay(make, dataset, env_cfg, mean_limit):
     cases.case_autoreset_replay(make, dataset, env_cfg, B=48, K=1500, mean_limit=mean_limit, stride=3)
+
+
+def test_async_rollouts(make, dataset, env_cfg):
+    cases.case_async_rollouts(make, dataset, env_cfg, device="cuda:0", B=16)
+
+
+def test_render_history_device(gpu_device, dataset, env_cfg):
+    from spark_sched_sim.env import SparkSchedSimEnv
+    from test_env_facade import check_render_history
+
+    from oracle.restatement import SparkSchedOracle
+
+    env = SparkSchedSimEnv(env_cfg, dataset, device=gpu_device, history_cap=1 << 16)
+    check_render_history(env, SparkSchedOracle(env_cfg, dataset))

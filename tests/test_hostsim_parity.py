@@ -56,3 +56,7 @@ def test_sampled_reset(make, dataset, env_cfg, cfg_over, B, seed0, mean_limit):
 @pytest.mark.parametrize("mean_limit", [None, 2.0e5])
 def test_autoreset_replay(make, dataset, env_cfg, mean_limit):
     cases.case_autoreset_replay(make, dataset, env_cfg, B=6, K=600, mean_limit=mean_limit)
+
+
+def test_async_rollouts(make, dataset, env_cfg):
+    cases.case_async_rollouts(make, dataset, env_cfg)

@@ -186,3 +186,16 @@ def test_ppo_iteration_gpu(gpu_device, dataset):
               device=gpu_device)
     hist = ppo.train(2, log=None)
     assert hist[-1]["samples"] > 100 and np.isfinite(hist[-1]["policy loss"])
+
+
+def test_ppo_async_rollouts_host(dataset):
+    """train_cfg["rollout_duration"] switches PPO to fixed-duration async rollouts (trainer.py:63,277-279):
+    episodes continue across iterations and are reset with per-row seed streams."""
+    from spark_sched_sim.trainers import PPO, AsyncRolloutCollector
+
+    ppo = PPO({"embed_dim": 16}, dict(SMALL_ENV, mean_time_limit=4e5), dict(TRAIN, rollout_duration=1.5e5),
+              engine_factory=_host_engine, dataset=dataset, device="cpu")
+    assert isinstance(ppo.collector, AsyncRolloutCollector)
+    hist = ppo.train(3, log=None)
+    assert len(hist) == 3 and all(np.isfinite(h["policy loss"]) for h in hist)
+    assert int(ppo.collector.reset_count.sum()) > 4  # at least one in-place reset after the first
