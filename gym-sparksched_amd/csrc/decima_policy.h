@@ -82,37 +82,44 @@ inline int64_t decima_policy_lds_bytes(int64_t node_cap, int64_t job_cap) { retu
 __device__ __forceinline__ float dp_leaky(float v) { return v >= 0.0f ? v : 0.2f * v; }
 
 // One lane's 3-layer MLP (act between layers, none after the last), weights via uniform addresses.
+// Packed layout per MLP (ssim_decima_policy): the FIRST layer's weight transposed ([IN][H1]) so the input loop
+// runs outermost over contiguous rows (each input is consumed once, only the H1 accumulators stay live);
+// layers 2 and 3 fused (each hidden-2 unit is activated and folded into the outputs at once, no H2 array).
+// Every sum runs in the same order as before (bias first, then ascending inputs), so the scores are
+// bit-identical to the unfused form.
 template <int IN, int H1, int H2, int OUT, bool kTanh>
 __device__ __forceinline__ void dp_mlp(const float* __restrict__ p, const float* in, float* out) {
-  const float* W0 = p;
-  const float* b0 = W0 + H1 * IN;
-  const float* W1 = b0 + H1;
+  const float* W0t = p;  // [IN][H1]
+  const float* b0 = W0t + H1 * IN;
+  const float* W1 = b0 + H1;  // [H2][H1]
   const float* b1 = W1 + H2 * H1;
-  const float* W2 = b1 + H2;
+  const float* W2 = b1 + H2;  // [OUT][H2]
   const float* b2 = W2 + OUT * H2;
   float a[H1];
 #pragma unroll
-  for (int j = 0; j < H1; ++j) {
-    float acc = b0[j];
+  for (int j = 0; j < H1; ++j) a[j] = b0[j];
+#pragma unroll 1
+  for (int i = 0; i < IN; ++i) {
+    const float v = in[i];
 #pragma unroll
-    for (int i = 0; i < IN; ++i) acc = __builtin_fmaf(W0[j * IN + i], in[i], acc);
-    a[j] = kTanh ? tanhf(acc) : dp_leaky(acc);
+    for (int j = 0; j < H1; ++j) a[j] = __builtin_fmaf(W0t[i * H1 + j], v, a[j]);
   }
-  float c[H2];
 #pragma unroll
-  for (int j = 0; j < H2; ++j) {
+  for (int j = 0; j < H1; ++j) a[j] = kTanh ? tanhf(a[j]) : dp_leaky(a[j]);
+  float o[OUT];
+#pragma unroll
+  for (int k = 0; k < OUT; ++k) o[k] = b2[k];
+#pragma unroll 1
+  for (int j = 0; j < H2; ++j) {  // not unrolled: one weight row (H1 floats) in SGPRs at a time
     float acc = b1[j];
 #pragma unroll
     for (int i = 0; i < H1; ++i) acc = __builtin_fmaf(W1[j * H1 + i], a[i], acc);
-    c[j] = kTanh ? tanhf(acc) : dp_leaky(acc);
+    const float c = kTanh ? tanhf(acc) : dp_leaky(acc);
+#pragma unroll
+    for (int k = 0; k < OUT; ++k) o[k] = __builtin_fmaf(W2[k * H2 + j], c, o[k]);
   }
 #pragma unroll
-  for (int k = 0; k < OUT; ++k) {
-    float acc = b2[k];
-#pragma unroll
-    for (int i = 0; i < H2; ++i) acc = __builtin_fmaf(W2[k * H2 + i], c[i], acc);
-    out[k] = acc;
-  }
+  for (int k = 0; k < OUT; ++k) out[k] = o[k];
 }
 
 // Gumbel(0,1) noise from a counter-based stream (splitmix64 of seed, env, counter, item).

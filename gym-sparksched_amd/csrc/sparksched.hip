@@ -54,8 +54,18 @@ __global__ __launch_bounds__(64) void k_reset_sampled(const Params* __restrict__
 
 // kRes: hot block LDS-resident. A compile-time flag (not a runtime select between an LDS and an HBM pointer)
 // so every hot-block access compiles to ds_read/ds_write rather than FLAT instructions.
+// Waves per SIMD the HBM-resident (kRes = false) kernels are compiled for. Their state lives in HBM, so the
+// event loop is bound by memory latency and occupancy hides it; the LDS-resident ones run one wave per SIMD
+// by LDS budget anyway. Register caps: 2 waves -> 256 VGPRs, 4 -> 128. Measured on the configs[3] shard (4096
+// envs, J=200, N=100): 8.9M decisions/s at 1 wave (266 VGPRs), 15.2M at 2, 17.3M at 4 (despite scratch spills).
+#ifndef SSIM_HBM_ROLLOUT_WAVES
+#define SSIM_HBM_ROLLOUT_WAVES 4
+#endif
+#ifndef SSIM_HBM_STEP_WAVES
+#define SSIM_HBM_STEP_WAVES 4
+#endif
 template <bool kRes, int kN, int kJ, int kS>
-__global__ __launch_bounds__(64) void k_step(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_STEP_WAVES))) void k_step(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                              const int32_t* __restrict__ stage_idx,
                                              const int32_t* __restrict__ num_exec) {
   const int eid = blockIdx.x;
@@ -82,7 +92,7 @@ __global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, con
 }
 
 template <bool kRes, int kN, int kJ, int kS>
-__global__ __launch_bounds__(64) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_ROLLOUT_WAVES))) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                 int kind, uint64_t seed, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
                                                 int32_t* action_log, uint64_t* prof_out, int64_t budget) {

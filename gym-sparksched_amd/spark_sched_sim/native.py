@@ -8,7 +8,8 @@ import os
 from ._abi import SsimConfig, SsimDataset, SsimLayout
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "libsparksched.so")
+# SSIM_LIB overrides the path (development A/B runs of alternative builds of the same sources)
+LIB_PATH = os.environ.get("SSIM_LIB") or os.path.join(os.path.dirname(_HERE), "build", "libsparksched.so")
 
 _lib = None
 

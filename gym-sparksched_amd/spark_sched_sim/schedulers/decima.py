@@ -404,6 +404,13 @@ class DecimaScheduler(nn.Module):
                 "exec_idx": exec_idx, "lgprob": (lg_stage + lg_exec).float()}
 
     @torch.no_grad()
+    def packed_params(self, dev) -> torch.Tensor:
+        """fp32 parameters in parameters() order for ssim_decima_policy, each MLP's first-layer weight
+        transposed to [in][out] (the kernel's input-outer loop reads contiguous rows)."""
+        return torch.cat([(p.detach().t() if n.endswith(".0.weight") else p.detach()).reshape(-1).float()
+                          for n, p in self.named_parameters()]).to(dev).contiguous()
+
+    @torch.no_grad()
     def schedule_fused(self, engine, feats: dict | None = None, seed: int = 0, counter: int = 0,
                        env_mask: torch.Tensor | None = None, node_cap: int | None = None,
                        with_scores: bool = False) -> dict[str, torch.Tensor]:
@@ -421,7 +428,7 @@ class DecimaScheduler(nn.Module):
         dev = eng.device
         if feats is None:
             feats = eng.decima_features()
-        params = torch.cat([p.detach().reshape(-1).float() for p in self.parameters()]).to(dev).contiguous()
+        params = self.packed_params(dev)
         if node_cap is None:
             node_cap = int(eng.views["counts"][:, _abi.OC_NUM_NODES].max().item())
         i32 = dict(dtype=torch.int32, device=dev)
