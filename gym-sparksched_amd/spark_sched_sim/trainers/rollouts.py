@@ -107,9 +107,10 @@ class RolloutCollector:
         f = {k: torch.from_numpy(x).to(dev) for k, x in eng.decima_features_np(*self.scales).items()}
         return v, f
 
-    def _decide_and_step(self, alive: torch.Tensor, generator=None):
+    def _decide_and_step(self, alive: torch.Tensor, generator=None, all_alive: bool = False):
         """One batched decision for the `alive` envs (the others get an invalid action and stay untouched),
-        then one engine step. Returns (live env ids, their observations as a DagBatch, action dict, views)."""
+        then one engine step. Returns (live env ids, their observations as a DagBatch, action dict, views).
+        `all_alive` (known to the caller): the full batch already is the live envs' batch (no re-selection)."""
         eng = self.engine
         v, f = self._views()
         b_all = build_batch(v, f, env_mask=alive)
@@ -122,7 +123,7 @@ class RolloutCollector:
         else:
             act = self.policy.schedule(b_all, generator=generator)
         envs = torch.nonzero(alive).squeeze(1)
-        batch = select_envs(b_all, envs)
+        batch = b_all if all_alive else select_envs(b_all, envs)
         si = torch.where(alive, act["stage_idx"], torch.full_like(act["stage_idx"], -2))
         if self.on_device:
             eng.step(si, act["num_exec"])
@@ -151,9 +152,10 @@ class RolloutCollector:
         alive = torch.ones(B, dtype=torch.bool, device=dev)
         wall = torch.zeros(B, dtype=torch.float64, device=dev)
         for _ in range(max_steps):
-            if not bool(alive.any()):
+            n_alive = int(alive.sum())
+            if n_alive == 0:
                 break
-            envs, batch, act, v = self._decide_and_step(alive, generator)
+            envs, batch, act, v = self._decide_and_step(alive, generator, all_alive=n_alive == B)
             reward = v["reward"][envs].double()
             buf.add(batch, envs, act, reward, wall[envs])
             wall = torch.where(alive, v["wall_time"].double(), wall)
@@ -210,9 +212,10 @@ class AsyncRolloutCollector(RolloutCollector):
         step = torch.zeros(B, dtype=torch.long, device=dev)
         alive = elapsed < self.rollout_duration
         for _ in range(max_steps):
-            if not bool(alive.any()):
+            n_alive = int(alive.sum())
+            if n_alive == 0:
                 break
-            envs, batch, act, v = self._decide_and_step(alive, generator)
+            envs, batch, act, v = self._decide_and_step(alive, generator, all_alive=n_alive == B)
             reward = v["reward"][envs].double()
             buf.add(batch, envs, act, reward, elapsed[envs])
             new_wall = v["wall_time"].double()

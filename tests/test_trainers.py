@@ -199,3 +199,25 @@ def test_ppo_async_rollouts_host(dataset):
     hist = ppo.train(3, log=None)
     assert len(hist) == 3 and all(np.isfinite(h["policy loss"]) for h in hist)
     assert int(ppo.collector.reset_count.sum()) > 4  # at least one in-place reset after the first
+
+
+def test_select_all_envs_is_identity(dataset):
+    """The rollout collectors skip select_envs when every env is alive: selecting all rows in order must
+    reproduce the full batch field by field."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.schedulers.decima import build_batch, select_envs
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0)
+    eng = _host_engine(cfg, 5, dataset)
+    eng.reset(seeds=list(range(5)))
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 3, 30)
+    v = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.host_views().items() if k != "trace"}
+    f = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.decima_features_np().items()}
+    full = build_batch(v, f, env_mask=torch.ones(5, dtype=torch.bool))
+    sel = select_envs(full, torch.arange(5))
+    for name in full.__dataclass_fields__ if hasattr(full, "__dataclass_fields__") else vars(full):
+        a, b = getattr(full, name), getattr(sel, name)
+        if isinstance(a, torch.Tensor):
+            assert a.dtype == b.dtype and torch.equal(a, b), name
+        else:
+            assert a == b, name
