@@ -70,8 +70,8 @@ __host__ __device__ inline DpLds dp_lds(int64_t cap, int64_t job_cap) {
   b = align16(b + cap * 2);
   o.flag = b;
   b = align16(b + cap);
-  o.hdag = b;
-  b += job_cap * kDpEmb * 4;
+  o.hdag = b;  // one row per active job: a job with no active stage is complete, so #jobs <= #nodes <= cap
+  b += (job_cap < cap ? job_cap : cap) * kDpEmb * 4;
   o.glob = b;
   b += kDpEmb * 4;
   o.total = align16(b);
