@@ -113,17 +113,20 @@ class RolloutCollector:
         `all_alive` (known to the caller): the full batch already is the live envs' batch (no re-selection)."""
         eng = self.engine
         v, f = self._views()
-        b_all = build_batch(v, f, env_mask=alive)
+        envs = torch.nonzero(alive).squeeze(1)
         if self.on_device and self.fused:  # one fused kernel launch (ssim_decima_policy)
+            # the policy reads the obs arena itself: only the live envs' batch is built (for the buffer),
+            # and its size sync also yields the LDS node cap
+            batch = build_batch(v, f, envs=None if all_alive else envs)
             self.counter += 1
             fo = self.policy.schedule_fused(eng, f, seed=self.seed, counter=self.counter, env_mask=alive,
-                                            node_cap=int(b_all.num_nodes.max().item()))
+                                            node_cap=batch.max_nodes)
             act = {"stage_idx": fo["stage_idx"], "num_exec": fo["num_exec"], "job_idx": fo["job_idx"].long(),
                    "exec_idx": fo["exec_idx"].long(), "lgprob": fo["lgprob"]}
         else:
+            b_all = build_batch(v, f, env_mask=alive)
             act = self.policy.schedule(b_all, generator=generator)
-        envs = torch.nonzero(alive).squeeze(1)
-        batch = b_all if all_alive else select_envs(b_all, envs)
+            batch = b_all if all_alive else select_envs(b_all, envs)
         si = torch.where(alive, act["stage_idx"], torch.full_like(act["stage_idx"], -2))
         if self.on_device:
             eng.step(si, act["num_exec"])

@@ -23,10 +23,10 @@ def main():
     orig = col._decide_and_step
     tm = {"decide_and_step": 0.0}
 
-    def timed(alive, generator=None):
+    def timed(alive, generator=None, all_alive=False):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        out = orig(alive, generator)
+        out = orig(alive, generator, all_alive=all_alive)
         torch.cuda.synchronize()
         tm["decide_and_step"] += time.perf_counter() - t0
         return out
@@ -75,6 +75,13 @@ def main():
         col.collect(ppo._seeds(), ppo._time_limits(ppo._seeds()), generator=ppo.gen, max_steps=20)
         torch.cuda.synchronize()
     print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=15), flush=True)
+    # one whole PPO iteration: rollouts vs the update (trainer.py:85-162 split)
+    t0 = tick()
+    buf = ppo.collect()
+    t1 = tick()
+    ppo.train_on_rollouts(buf)
+    t2 = tick()
+    print(f"iteration: collect {t1 - t0:.2f} s ({len(buf)} samples), train_on_rollouts {t2 - t1:.2f} s", flush=True)
 
 
 if __name__ == "__main__":

@@ -221,3 +221,28 @@ def test_select_all_envs_is_identity(dataset):
             assert a.dtype == b.dtype and torch.equal(a, b), name
         else:
             assert a == b, name
+
+
+def test_build_batch_of_env_subset(dataset):
+    """build_batch(envs=...) (the fused rollout path: only live envs, one size sync) == select_envs of the
+    masked full batch, field by field, for a subset in arbitrary order."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.schedulers.decima import build_batch, select_envs
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0)
+    eng = _host_engine(cfg, 6, dataset)
+    eng.reset(seeds=list(range(6)))
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 5, 25)
+    v = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.host_views().items() if k != "trace"}
+    f = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.decima_features_np().items()}
+    alive = torch.tensor([True, False, True, True, False, True])
+    for envs in (torch.nonzero(alive).squeeze(1), torch.tensor([5, 0, 3]), torch.tensor([2])):
+        want = select_envs(build_batch(v, f, env_mask=alive), envs)
+        got = build_batch(v, f, envs=envs)
+        assert got.max_nodes == int(got.num_nodes.max()) > 0
+        for name in got.__dataclass_fields__:
+            a, b = getattr(want, name), getattr(got, name)
+            if isinstance(a, torch.Tensor):
+                assert a.dtype == b.dtype and torch.equal(a, b), name
+            else:
+                assert a == b, name
