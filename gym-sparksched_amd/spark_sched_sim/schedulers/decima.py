@@ -435,7 +435,7 @@ class DecimaScheduler(nn.Module):
     @torch.no_grad()
     def schedule_fused(self, engine, feats: dict | None = None, seed: int = 0, counter: int = 0,
                        env_mask: torch.Tensor | None = None, node_cap: int | None = None,
-                       with_scores: bool = False) -> dict[str, torch.Tensor]:
+                       with_scores: bool = False, params: torch.Tensor | None = None) -> dict[str, torch.Tensor]:
         """`schedule` for every env of a DeviceEngine in ONE kernel launch (ssim_decima_policy,
         csrc/decima_policy.h): the same forward over the obs arena and the device features, weights read
         from a packed copy of this module's parameters, sampling on a counter-based device stream of
@@ -450,7 +450,8 @@ class DecimaScheduler(nn.Module):
         dev = eng.device
         if feats is None:
             feats = eng.decima_features()
-        params = self.packed_params(dev)
+        if params is None:  # callers stepping many decisions with fixed weights pass packed_params() once
+            params = self.packed_params(dev)
         if node_cap is None:
             node_cap = int(eng.views["counts"][:, _abi.OC_NUM_NODES].max().item())
         i32 = dict(dtype=torch.int32, device=dev)

@@ -95,6 +95,7 @@ class RolloutCollector:
         self.seed = seed
         self.counter = 0
         self.on_device = isinstance(engine.views["counts"], torch.Tensor)  # DeviceEngine vs test host build
+        self._params = None  # packed policy weights, valid during one collect()
 
     def _views(self, features: bool = True):
         eng = self.engine
@@ -107,20 +108,25 @@ class RolloutCollector:
         f = {k: torch.from_numpy(x).to(dev) for k, x in eng.decima_features_np(*self.scales).items()}
         return v, f
 
-    def _decide_and_step(self, alive: torch.Tensor, generator=None, all_alive: bool = False):
+    def _decide_and_step(self, alive: torch.Tensor, generator=None, all_alive: bool = False,
+                         envs: torch.Tensor | None = None):
         """One batched decision for the `alive` envs (the others get an invalid action and stay untouched),
         then one engine step. Returns (live env ids, their observations as a DagBatch, action dict, views).
-        `all_alive` (known to the caller): the full batch already is the live envs' batch (no re-selection)."""
+        `all_alive` (known to the caller): the full batch already is the live envs' batch (no re-selection);
+        `envs` (optional): the caller's nonzero(alive)."""
         eng = self.engine
         v, f = self._views()
-        envs = torch.nonzero(alive).squeeze(1)
+        if envs is None:
+            envs = torch.nonzero(alive).squeeze(1)
         if self.on_device and self.fused:  # one fused kernel launch (ssim_decima_policy)
             # the policy reads the obs arena itself: only the live envs' batch is built (for the buffer),
             # and its size sync also yields the LDS node cap
             batch = build_batch(v, f, envs=None if all_alive else envs)
             self.counter += 1
+            if self._params is None:  # weights are fixed for a whole collect(): pack them once
+                self._params = self.policy.packed_params(eng.device)
             fo = self.policy.schedule_fused(eng, f, seed=self.seed, counter=self.counter, env_mask=alive,
-                                            node_cap=batch.max_nodes)
+                                            node_cap=batch.max_nodes, params=self._params)
             act = {"stage_idx": fo["stage_idx"], "num_exec": fo["num_exec"], "job_idx": fo["job_idx"].long(),
                    "exec_idx": fo["exec_idx"].long(), "lgprob": fo["lgprob"]}
         else:
@@ -144,6 +150,7 @@ class RolloutCollector:
     def collect(self, seeds, time_limits=None, generator=None, max_steps: int = 10**9) -> GpuRolloutBuffer:
         """RolloutWorkerSync.collect_rollout (rollout_worker.py:135-157): reset every env with its seed,
         step until each env's episode ends."""
+        self._params = None  # re-pack the (possibly updated) policy weights
         eng = self.engine
         B = eng.num_envs
         limits = None if time_limits is None else torch.as_tensor(time_limits, dtype=torch.float64)
@@ -155,10 +162,10 @@ class RolloutCollector:
         alive = torch.ones(B, dtype=torch.bool, device=dev)
         wall = torch.zeros(B, dtype=torch.float64, device=dev)
         for _ in range(max_steps):
-            n_alive = int(alive.sum())
-            if n_alive == 0:
+            envs = torch.nonzero(alive).squeeze(1)  # the loop's one size sync
+            if envs.numel() == 0:
                 break
-            envs, batch, act, v = self._decide_and_step(alive, generator, all_alive=n_alive == B)
+            envs, batch, act, v = self._decide_and_step(alive, generator, all_alive=envs.numel() == B, envs=envs)
             reward = v["reward"][envs].double()
             buf.add(batch, envs, act, reward, wall[envs])
             wall = torch.where(alive, v["wall_time"].double(), wall)
@@ -202,6 +209,7 @@ class AsyncRolloutCollector(RolloutCollector):
 
     @torch.no_grad()
     def collect(self, generator=None, max_steps: int = 10**9) -> GpuRolloutBuffer:
+        self._params = None  # re-pack the (possibly updated) policy weights
         B = self.engine.num_envs
         if self.next_wall is None:  # first call: reset every worker (rollout_worker.py:174-176)
             self._reset(np.arange(B))
@@ -215,10 +223,10 @@ class AsyncRolloutCollector(RolloutCollector):
         step = torch.zeros(B, dtype=torch.long, device=dev)
         alive = elapsed < self.rollout_duration
         for _ in range(max_steps):
-            n_alive = int(alive.sum())
-            if n_alive == 0:
+            envs = torch.nonzero(alive).squeeze(1)  # the loop's one size sync
+            if envs.numel() == 0:
                 break
-            envs, batch, act, v = self._decide_and_step(alive, generator, all_alive=n_alive == B)
+            envs, batch, act, v = self._decide_and_step(alive, generator, all_alive=envs.numel() == B, envs=envs)
             reward = v["reward"][envs].double()
             buf.add(batch, envs, act, reward, elapsed[envs])
             new_wall = v["wall_time"].double()

@@ -23,10 +23,10 @@ def main():
     orig = col._decide_and_step
     tm = {"decide_and_step": 0.0}
 
-    def timed(alive, generator=None, all_alive=False):
+    def timed(alive, generator=None, **kw):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        out = orig(alive, generator, all_alive=all_alive)
+        out = orig(alive, generator, **kw)
         torch.cuda.synchronize()
         tm["decide_and_step"] += time.perf_counter() - t0
         return out
