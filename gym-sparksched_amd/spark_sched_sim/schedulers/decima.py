@@ -97,11 +97,13 @@ def _expand(counts: torch.Tensor, total: int):
 
 
 def build_batch(views: dict, feats: dict, env_mask: torch.Tensor | None = None,
-                envs: torch.Tensor | None = None) -> DagBatch:
+                envs: torch.Tensor | None = None, sizes: tuple[int, int, int, int, int] | None = None) -> DagBatch:
     """Flat batch from the obs-arena views (DeviceEngine.views) and the device Decima features
     (DeviceEngine.decima_features). `env_mask` (bool [B]) empties envs (e.g. finished ones). `envs` (i64 [K])
     builds the batch of just those envs, renumbered 0..K-1 in the given order: the same batch as
-    `select_envs(build_batch(views, feats), envs)` in one pass (one host sync instead of two)."""
+    `select_envs(build_batch(views, feats), envs)` in one pass (one host sync instead of two). `sizes`
+    (total nodes, edges, DAGs, max levels, max nodes of the batch), when the caller already has them on the
+    host (`live_sizes`), removes the remaining sync."""
     c = views["counts"]
     dev = c.device
     rows = None
@@ -119,7 +121,9 @@ def build_batch(views: dict, feats: dict, env_mask: torch.Tensor | None = None,
         n, ne, nj = n * keep, ne * keep, nj * keep
     depth = feats["depth"] if rows is None else feats["depth"][rows]
     levels = torch.clamp(depth.long() - 1, min=0) * (n > 0)
-    if B == 0:
+    if sizes is not None:
+        Nt, Et, Gt, L, Nmax = sizes
+    elif B == 0:
         Nt = Et = Gt = L = Nmax = 0
     else:
         Nt, Et, Gt, L, Nmax = (int(v) for v in torch.stack([n.sum(), ne.sum(), nj.sum(), levels.max(),
@@ -145,6 +149,22 @@ def build_batch(views: dict, feats: dict, env_mask: torch.Tensor | None = None,
                     ptr=_ptr(dag_counts), node_dag=node_dag, node_env=node_env, dag_env=dag_env, obs_ptr=_ptr(nj),
                     stage_mask=stage_mask, exec_cap=feats["commit_cap"][dag_src, dl].long(),
                     num_stage_acts=num_stage_acts, num_nodes=n, num_edges=ne, num_envs=B, max_nodes=Nmax)
+
+
+def live_sizes(views: dict, feats: dict, alive: torch.Tensor):
+    """One host sync for a rollout step: the live env ids (device i64, ascending, via nonzero_static) and the
+    `sizes` tuple build_batch(views, feats, envs=ids) needs. Returns (ids, sizes) with ids empty if none."""
+    c = views["counts"]
+    st = torch.stack([alive.to(c.device).long(), c[:, _abi.OC_NUM_NODES].long(), c[:, _abi.OC_NUM_EDGES].long(),
+                      c[:, _abi.OC_NUM_JOBS].long(), feats["depth"].long()]).cpu()
+    live = st[0] != 0
+    k = int(live.sum())
+    ids = torch.nonzero_static(alive.to(c.device), size=k).squeeze(1)
+    if k == 0:
+        return ids, (0, 0, 0, 0, 0)
+    n, ne, nj, d = st[1][live], st[2][live], st[3][live], st[4][live]
+    levels = torch.clamp(d - 1, min=0) * (n > 0)
+    return ids, (int(n.sum()), int(ne.sum()), int(nj.sum()), int(levels.max()), int(n.max()))
 
 
 def select_envs(b: DagBatch, envs: torch.Tensor) -> DagBatch:

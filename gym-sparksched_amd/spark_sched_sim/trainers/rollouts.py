@@ -15,7 +15,7 @@ import torch
 
 from .. import _abi
 from ..wrappers import StochasticTimeLimitSampler
-from ..schedulers.decima import DagBatch, build_batch, cat_batches, select_envs
+from ..schedulers.decima import live_sizes, DagBatch, build_batch, cat_batches, select_envs
 
 
 class GpuRolloutBuffer:
@@ -96,6 +96,7 @@ class RolloutCollector:
         self.counter = 0
         self.on_device = isinstance(engine.views["counts"], torch.Tensor)  # DeviceEngine vs test host build
         self._params = None  # packed policy weights, valid during one collect()
+        self._pre = None  # (views, feats, live ids, batch sizes) fetched by _live for the next step
 
     def _views(self, features: bool = True):
         eng = self.engine
@@ -115,13 +116,18 @@ class RolloutCollector:
         `all_alive` (known to the caller): the full batch already is the live envs' batch (no re-selection);
         `envs` (optional): the caller's nonzero(alive)."""
         eng = self.engine
-        v, f = self._views()
+        if self._pre is not None:  # views, features and live sizes already fetched by the loop (live())
+            v, f, envs, sizes = self._pre
+            self._pre = None
+        else:
+            v, f = self._views()
+            sizes = None
         if envs is None:
             envs = torch.nonzero(alive).squeeze(1)
         if self.on_device and self.fused:  # one fused kernel launch (ssim_decima_policy)
             # the policy reads the obs arena itself: only the live envs' batch is built (for the buffer),
-            # and its size sync also yields the LDS node cap
-            batch = build_batch(v, f, envs=None if all_alive else envs)
+            # its sizes (from the loop's one sync) also give the LDS node cap
+            batch = build_batch(v, f, envs=None if all_alive else envs, sizes=sizes)
             self.counter += 1
             if self._params is None:  # weights are fixed for a whole collect(): pack them once
                 self._params = self.policy.packed_params(eng.device)
@@ -140,6 +146,17 @@ class RolloutCollector:
             eng.step(si.cpu().numpy(), act["num_exec"].cpu().numpy())
         v, _ = self._views(features=False)
         return envs, batch, act, v
+
+    def _live(self, alive: torch.Tensor) -> torch.Tensor:
+        """Live env ids for the next decision. Device fused path: the step's single host sync (live_sizes),
+        with the views/features kept for _decide_and_step; otherwise a plain nonzero."""
+        if self.on_device and self.fused:
+            v, f = self._views()
+            envs, sizes = live_sizes(v, f, alive)
+            self._pre = (v, f, envs, sizes)
+            return envs
+        self._pre = None
+        return torch.nonzero(alive).squeeze(1)
 
     @staticmethod
     def _done(v) -> torch.Tensor:
@@ -162,7 +179,7 @@ class RolloutCollector:
         alive = torch.ones(B, dtype=torch.bool, device=dev)
         wall = torch.zeros(B, dtype=torch.float64, device=dev)
         for _ in range(max_steps):
-            envs = torch.nonzero(alive).squeeze(1)  # the loop's one size sync
+            envs = self._live(alive)  # the loop's one size sync
             if envs.numel() == 0:
                 break
             envs, batch, act, v = self._decide_and_step(alive, generator, all_alive=envs.numel() == B, envs=envs)
@@ -223,7 +240,7 @@ class AsyncRolloutCollector(RolloutCollector):
         step = torch.zeros(B, dtype=torch.long, device=dev)
         alive = elapsed < self.rollout_duration
         for _ in range(max_steps):
-            envs = torch.nonzero(alive).squeeze(1)  # the loop's one size sync
+            envs = self._live(alive)  # the loop's one size sync
             if envs.numel() == 0:
                 break
             envs, batch, act, v = self._decide_and_step(alive, generator, all_alive=envs.numel() == B, envs=envs)

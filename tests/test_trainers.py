@@ -246,3 +246,30 @@ def test_build_batch_of_env_subset(dataset):
                 assert a.dtype == b.dtype and torch.equal(a, b), name
             else:
                 assert a == b, name
+
+
+def test_live_sizes_match_build_batch(dataset):
+    """live_sizes (the fused rollout step's single host sync) gives the live ids and exactly the sizes
+    build_batch(envs=ids) would sync for; passing them builds the identical batch."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.schedulers.decima import build_batch, live_sizes
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0)
+    eng = _host_engine(cfg, 6, dataset)
+    eng.reset(seeds=list(range(6)))
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 7, 20)
+    v = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.host_views().items() if k != "trace"}
+    f = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.decima_features_np().items()}
+    for alive in (torch.tensor([True, False, True, True, False, True]), torch.ones(6, dtype=torch.bool),
+                  torch.zeros(6, dtype=torch.bool)):
+        ids, sizes = live_sizes(v, f, alive)
+        assert torch.equal(ids, torch.nonzero(alive).squeeze(1))
+        if ids.numel() == 0:
+            assert sizes == (0, 0, 0, 0, 0)
+            continue
+        ref = build_batch(v, f, envs=ids)
+        assert sizes == (ref.x.shape[0], ref.edge_index.shape[1], ref.ptr.numel() - 1, ref.max_levels, ref.max_nodes)
+        got = build_batch(v, f, envs=ids, sizes=sizes)
+        for name in got.__dataclass_fields__:
+            a, b = getattr(ref, name), getattr(got, name)
+            assert (torch.equal(a, b) if isinstance(a, torch.Tensor) else a == b), name
