@@ -245,6 +245,7 @@ def main():
         pol = DecimaScheduler(cfg["num_executors"]).to(dev)  # decima_tpch.yaml:66-78 dims, random init
         gen = torch.Generator(device=dev).manual_seed(args.seed)
         cnt = eng.views["counts"]
+        packed = pol.packed_params(dev)  # fixed weights during rollouts: packed once, like RolloutCollector
 
     def chunks(n):
         return [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
@@ -266,7 +267,8 @@ def main():
                     act = pol.schedule(build_batch(eng.views, eng.decima_features()), generator=gen)
                 else:  # one fused HIP launch (ssim_decima_policy)
                     run.counter += 1
-                    act = pol.schedule_fused(eng, eng.decima_features(), seed=args.seed, counter=run.counter)
+                    act = pol.schedule_fused(eng, eng.decima_features(), seed=args.seed, counter=run.counter,
+                                             params=packed)
                 if events is not None:
                     events[2 * k].record(stream)
                 eng.step(act["stage_idx"], act["num_exec"])
