@@ -200,24 +200,45 @@ def select_envs(b: DagBatch, envs: torch.Tensor) -> DagBatch:
 
 
 def cat_batches(bs: list[DagBatch]) -> DagBatch:
-    """Concatenation of batches (observations in list order)."""
+    """Concatenation of batches (observations in list order). Index fields are shifted by per-element
+    offsets expanded with repeat_interleave, so the cost is a fixed number of launches per field rather than
+    one per batch (a rollout buffer holds thousands of per-step batches)."""
     dev = bs[0].x.device
-    n_off = torch.tensor([0] + [b.x.shape[0] for b in bs], device=dev).cumsum(0)
-    g_off = torch.tensor([0] + [b.ptr.numel() - 1 for b in bs], device=dev).cumsum(0)
-    e_off = torch.tensor([0] + [b.num_envs for b in bs], device=dev).cumsum(0)
+    i64 = dict(dtype=torch.long, device=dev)
+    nN = [b.x.shape[0] for b in bs]
+    nE = [b.edge_index.shape[1] for b in bs]
+    nG = [b.ptr.numel() - 1 for b in bs]
+    nB = [b.num_envs for b in bs]
+
+    def offsets(counts):  # exclusive prefix sums (host)
+        out, t = [], 0
+        for c in counts:
+            out.append(t)
+            t += c
+        return torch.tensor(out, **i64), t
+
+    n_off, Nt = offsets(nN)
+    g_off, Gt = offsets(nG)
+    e_off, Bt = offsets(nB)
+    Et = sum(nE)
+
+    def per_item(off, counts, total):  # offset of each element's batch
+        return torch.repeat_interleave(off, torch.tensor(counts, **i64), output_size=total)
+
+    zero = torch.zeros(1, **i64)
     return DagBatch(
         x=torch.cat([b.x for b in bs]),
-        edge_index=torch.cat([b.edge_index + n_off[i] for i, b in enumerate(bs)], dim=1),
+        edge_index=torch.cat([b.edge_index for b in bs], dim=1) + per_item(n_off, nE, Et)[None, :],
         edge_bits=torch.cat([b.edge_bits for b in bs]),
         max_levels=max(b.max_levels for b in bs), env_levels=torch.cat([b.env_levels for b in bs]),
-        ptr=torch.cat([bs[0].ptr[:1]] + [b.ptr[1:] + n_off[i] for i, b in enumerate(bs)]),
-        node_dag=torch.cat([b.node_dag + g_off[i] for i, b in enumerate(bs)]),
-        node_env=torch.cat([b.node_env + e_off[i] for i, b in enumerate(bs)]),
-        dag_env=torch.cat([b.dag_env + e_off[i] for i, b in enumerate(bs)]),
-        obs_ptr=torch.cat([bs[0].obs_ptr[:1]] + [b.obs_ptr[1:] + g_off[i] for i, b in enumerate(bs)]),
+        ptr=torch.cat([bs[0].ptr[:1]] + [b.ptr[1:] for b in bs]) + torch.cat([zero, per_item(n_off, nG, Gt)]),
+        node_dag=torch.cat([b.node_dag for b in bs]) + per_item(g_off, nN, Nt),
+        node_env=torch.cat([b.node_env for b in bs]) + per_item(e_off, nN, Nt),
+        dag_env=torch.cat([b.dag_env for b in bs]) + per_item(e_off, nG, Gt),
+        obs_ptr=torch.cat([bs[0].obs_ptr[:1]] + [b.obs_ptr[1:] for b in bs]) + torch.cat([zero, per_item(g_off, nB, Bt)]),
         stage_mask=torch.cat([b.stage_mask for b in bs]), exec_cap=torch.cat([b.exec_cap for b in bs]),
         num_stage_acts=torch.cat([b.num_stage_acts for b in bs]), num_nodes=torch.cat([b.num_nodes for b in bs]),
-        num_edges=torch.cat([b.num_edges for b in bs]), num_envs=int(sum(b.num_envs for b in bs)),
+        num_edges=torch.cat([b.num_edges for b in bs]), num_envs=int(Bt),
         max_nodes=max(b.max_nodes for b in bs))
 
 

@@ -82,6 +82,20 @@ def main():
     ppo.train_on_rollouts(buf)
     t2 = tick()
     print(f"iteration: collect {t1 - t0:.2f} s ({len(buf)} samples), train_on_rollouts {t2 - t1:.2f} s", flush=True)
+    # learn split: trajectories/returns/baseline, samples() (cat of the per-step batches), the PPO epochs
+    buf = ppo.collect()
+    t0 = tick()
+    times, rewards, lengths, sample = buf.trajectories()
+    returns = ppo.return_calc(times, rewards, lengths)
+    ppo.baseline(times[:, :-1], returns, lengths)
+    t1 = tick()
+    obs, acts = buf.samples()
+    t2 = tick()
+    advg = torch.zeros(len(buf), dtype=torch.float32, device=obs.x.device)
+    ppo._train(obs, acts, advg)
+    t3 = tick()
+    print(f"learn split: returns+baseline {t1 - t0:.3f} s, samples() {t2 - t1:.3f} s, epochs {t3 - t2:.3f} s",
+          flush=True)
 
 
 if __name__ == "__main__":

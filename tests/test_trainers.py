@@ -273,3 +273,25 @@ def test_live_sizes_match_build_batch(dataset):
         for name in got.__dataclass_fields__:
             a, b = getattr(ref, name), getattr(got, name)
             assert (torch.equal(a, b) if isinstance(a, torch.Tensor) else a == b), name
+
+
+def test_cat_batches_equals_select_of_all(dataset):
+    """cat_batches of per-env (and mixed-size, incl. empty) sub-batches == select_envs of the same envs at
+    once, every field bit for bit (the rollout buffer concatenates thousands of per-step batches this way)."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.schedulers.decima import build_batch, cat_batches, select_envs
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0)
+    eng = _host_engine(cfg, 6, dataset)
+    eng.reset(seeds=list(range(6)))
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 9, 30)
+    v = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.host_views().items() if k != "trace"}
+    f = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.decima_features_np().items()}
+    full = build_batch(v, f)
+    order = torch.tensor([3, 0, 5, 1, 4, 2, 0])
+    want = select_envs(full, order)
+    for parts in ([order[k:k + 1] for k in range(7)], [order[:2], order[2:2], order[2:6], order[6:]]):
+        got = cat_batches([select_envs(full, p) for p in parts])
+        for name in got.__dataclass_fields__:
+            a, b = getattr(want, name), getattr(got, name)
+            assert (a.dtype == b.dtype and torch.equal(a, b)) if isinstance(a, torch.Tensor) else a == b, name
