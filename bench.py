@@ -2,16 +2,26 @@
 """Scheduling decisions/sec on BASELINE.json configs[1]: 1024 TPC-H-format envs per GPU, 50 jobs /
 10 executors, uniform-random valid actions from the device RNG (the reference's examples.py ENV_CFG).
 
-A "step" = one env.step for every env of the batch: device random policy reads the obs, then the step
-kernel applies the action, runs the discrete-event loop and writes the next observation to HBM.
-Modes: `rollout` (default: K steps = K x envs decisions of policy+step fused into one launch, the decisions
-claimed from a shared budget so that envs with cheap decisions take more and the launch has no tail;
-`--lockstep` gives every env exactly K; `--compare-lockstep` times one lockstep launch off the clock beside
-the budget launch) and
-`step` (two launches per step, the C-ABI call pattern of an external policy).
+A "step" = one env.step for every env of the batch: the device random policy reads the env's observation,
+then the step applies the action, runs the discrete-event loop and writes the next observation to HBM.
 
-Output: one JSON line on rank 0. Multi-GPU: one process per GPU (torchrun), envs sharded per rank with
-no data-path collective (weak scaling); decisions are summed and time is max-reduced over ranks.
+Timeline of one run (all launches on one stream, inputs resident in HBM before anything is timed):
+  1. reset every env on the device (ssim_reset_sampled, seeds = global env ids);
+  2. pre-roll (untimed, not warm-up): env i takes a seeded, uniformly random number of decisions in
+     [0, `preroll`) with auto-reset (ssim_rollout_steps), so the batch is spread over every phase of its
+     episodes — early, late and restarting — instead of all envs sitting at the same decision index;
+  3. warm-up: exactly `--warmup` steps (one launch of warmup x envs decisions);
+  4. timed: exactly `--steps` steps (launches of `--chunk` steps, default one), bracketed by barrier +
+     synchronize; HIP events on the launch stream time the kernels for the roofline.
+Modes: `rollout` (default: K steps = K x envs decisions of policy+step fused into one launch, claimed from a
+shared budget so envs with cheap decisions take more and the launch has no tail; `--lockstep` gives every env
+exactly K) and `step` (two launches per step, the C-ABI call pattern of an external policy).
+
+Multi-GPU: `--gpus N` with no torchrun environment spawns N worker processes itself (one per GPU, before any
+HIP call); under torchrun the environment is used as is. Envs are sharded in contiguous blocks per rank with no
+data-path collective (weak scaling); decisions are summed and time is max-reduced over ranks.
+
+Output: one JSON line on rank 0.
 """
 
 from __future__ import annotations
@@ -20,6 +30,7 @@ import argparse
 import json
 import multiprocessing as mp
 import os
+import subprocess
 import sys
 import time
 
@@ -30,69 +41,189 @@ for _p in (REPO, os.path.join(REPO, "gym-sparksched_amd")):
 
 ENV_CFG = {"num_executors": 10, "job_arrival_cap": 50, "job_arrival_rate": 4.0e-5, "moving_delay": 2000.0,
            "warmup_delay": 1000.0}  # examples.py:15-23
+DECIMA_ENV = {"num_executors": 50, "job_arrival_cap": 200, "job_arrival_rate": 4.0e-5, "moving_delay": 2000.0,
+              "warmup_delay": 1000.0}  # config/decima_tpch.yaml:80-87
+LARGE_ENV = {"num_executors": 100, "job_arrival_cap": 200, "job_arrival_rate": 4.0e-5, "moving_delay": 2000.0,
+             "warmup_delay": 1000.0}
 # BASELINE.json configs: "tpch" = configs[1] (the metric's config, default), "decima" = configs[2] (Decima GNN
 # policy on the GPU vector env, env section of config/decima_tpch.yaml:80-87), "large" = configs[3]'s per-GPU
 # shard (4096 of the 32k envs, 200 jobs / 100 executors, Poisson arrivals, mean_time_limit 2e7 ms).
+# `preroll`: upper bound of the per-env pre-roll (about one episode of the workload's policy).
 WORKLOADS = {
-    "tpch": dict(cfg=ENV_CFG, envs=1024, mean_time_limit=None,
+    "tpch": dict(cfg=ENV_CFG, envs=1024, mean_time_limit=None, preroll=1000, policy="random",
                  desc="{B} envs/GPU x TPC-H 50 jobs / 10 executors, random valid actions (BASELINE configs[1])"),
-    "decima": dict(cfg={"num_executors": 50, "job_arrival_cap": 200, "job_arrival_rate": 4.0e-5,
-                        "moving_delay": 2000.0, "warmup_delay": 1000.0}, envs=4096, mean_time_limit=2.0e7,
-                   desc="{B} envs/GPU x TPC-H 200-job cap / 50 executors, Decima GNN policy (random init) in "
-                        "PyTorch-ROCm on device obs (BASELINE configs[2])"),
-    "ppo": dict(cfg=None, envs=16, mean_time_limit=2.0e7,
-                desc="full PPO iteration of config/decima_tpch.yaml per GPU ({B} rollouts = 4 job sequences x 4, "
-                     "Decima GNN, GPU rollouts, data-parallel replicas over RCCL) (BASELINE configs[4])"),
-    "large": dict(cfg={"num_executors": 100, "job_arrival_cap": 200, "job_arrival_rate": 4.0e-5,
-                       "moving_delay": 2000.0, "warmup_delay": 1000.0}, envs=4096, mean_time_limit=2.0e7,
+    "decima": dict(cfg=DECIMA_ENV, envs=4096, mean_time_limit=2.0e7, preroll=1500, policy="decima",
+                   desc="{B} envs/GPU x TPC-H 200-job cap / 50 executors, Decima GNN policy (random init) on "
+                        "device obs (BASELINE configs[2])"),
+    "ppo": dict(cfg=DECIMA_ENV, envs=16, mean_time_limit=2.0e7, preroll=0, policy="decima",
+                desc="full PPO iteration of config/decima_tpch.yaml ({B} rollouts = 4 job sequences x 4, Decima "
+                     "GNN, GPU rollouts, trajectories gathered to one learner over RCCL) (BASELINE configs[4])"),
+    "large": dict(cfg=LARGE_ENV, envs=4096, mean_time_limit=2.0e7, preroll=3000, policy="random",
                   desc="{B} envs/GPU x TPC-H 200-job cap / 100 executors, Poisson arrivals, time limits, random "
                        "valid actions (BASELINE configs[3] per-GPU shard)"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
+# ------------------------------------------------------------------------------------------------ launcher
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus N` without a torchrun environment: one worker process per GPU (trainer.py:264-296 fans out
+    rollout processes the same way), started BEFORE this process touches HIP. Returns the worst exit code."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:  # one rank failed: the collectives of the others would hang
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+# ------------------------------------------------------------------------------------------------ CPU baseline
+def usable_cpus() -> int:
+    """CPUs this process may run on: the affinity mask, capped by a cgroup-v2 CPU quota (the GPU box gives a
+    job a share of the host's cores; os.cpu_count() reports the whole host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def _cpu_worker(args):
-    """One reference-style rollout worker (trainers/rollout_worker.py:53-95): one env per process,
-    torch.set_num_threads(1)-equivalent single thread, RandomScheduler(seed), episodes back to back."""
-    seed, seconds = args
+    """One reference-style rollout worker (trainers/rollout_worker.py:53-95): one env per process, single
+    thread, episodes back to back with the workload's policy; warm-up = the first episode (at most
+    `warm_s` seconds), then decisions are counted for `seconds` of wall time."""
+    workload, seed, seconds, warm_s = args
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "gym-sparksched_amd"))
-    from oracle.policies import RandomPolicy
+    import numpy as np
+
+    from oracle.policies import FairPolicy, RandomPolicy
     from oracle.restatement import SparkSchedOracle
     from spark_sched_sim.data_samplers.synthetic_tpch import generate
+    from spark_sched_sim.wrappers import StochasticTimeLimit
 
-    ds = generate(0)
-    env = SparkSchedOracle(ENV_CFG, ds)
-    pol = RandomPolicy(42 + seed)
-    env.reset(seed=seed)  # warm-up episode start (not counted)
-    decisions, t0, ep = 0, time.perf_counter(), 0
+    try:
+        import torch
+
+        torch.set_num_threads(1)  # rollout_worker.py:93
+    except ImportError:
+        torch = None
+    wl = WORKLOADS[workload]
+    cfg = wl["cfg"]
+    env = SparkSchedOracle(cfg, generate(0))
+    if wl["mean_time_limit"]:
+        env = StochasticTimeLimit(env, wl["mean_time_limit"])
+    if wl["policy"] == "decima":
+        from oracle import decima as D
+        from oracle import decima_gnn as G
+        from spark_sched_sim.schedulers.decima import DecimaScheduler
+
+        torch.manual_seed(seed)
+        sd = {k: v.detach().float() for k, v in DecimaScheduler(cfg["num_executors"]).state_dict().items()}
+        rng = np.random.default_rng(seed)
+        N = cfg["num_executors"]
+
+        def act(obs):  # DecimaScheduler.schedule (scheduler.py:71-99) on the wrapped observation
+            ro = D.decima_observation(obs, N)
+            if not ro["stage_mask"].any():
+                return {"stage_idx": -1, "num_exec": max(1, obs["num_committable_execs"])}
+            with torch.no_grad():
+                enc = G.encode(sd, ro)
+                s = G.stage_scores(sd, ro, enc).numpy()
+                si = int(np.argmax(s - np.log(-np.log(rng.random(s.shape)))))
+                j = G.job_of_stage(ro, si)
+                e = G.exec_scores(sd, ro, enc, j, N).numpy()
+                ei = int(np.argmax(e - np.log(-np.log(rng.random(e.shape)))))
+            return {"stage_idx": si, "num_exec": 1 + ei}  # DecimaActWrapper.action (env_wrapper.py:33-34)
+    else:
+        pol = FairPolicy(cfg["num_executors"]) if wl["policy"] == "fair" else RandomPolicy(42 + seed)
+
+        def act(obs):
+            return pol.schedule(obs)[0]
+    ep = 0
     obs, _ = env.reset(seed=seed)
+    t_w = time.perf_counter()
+    while time.perf_counter() - t_w < warm_s:  # warm-up: one episode (bounded)
+        obs, _, term, trunc, _ = env.step(act(obs))
+        if term or trunc:
+            break
+    ep += 1
+    obs, _ = env.reset(seed=seed + 1000 * ep)
+    decisions, episodes, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        a, _ = pol.schedule(obs)
-        obs, _, done, _, _ = env.step(a)
+        obs, _, term, trunc, _ = env.step(act(obs))
         decisions += 1
-        if done:
+        if term or trunc:
             ep += 1
+            episodes += 1
             obs, _ = env.reset(seed=seed + 1000 * ep)
-    return decisions, time.perf_counter() - t0
+    return decisions, time.perf_counter() - t0, episodes
 
 
-def cpu_baseline(seconds: float, procs: int) -> dict:
+def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0) -> dict:
+    """The reference's CPU rollout path, timed on this host's cores: the oracle restatement (same CPython
+    dict/set/heapq and numpy Generator machinery as spark_sched_sim) in `procs` spawn processes, one env each,
+    harness shaped like trainers/rollout_worker.py:53-95."""
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(7 + i, seconds) for i in range(procs)])
+        res = pool.map(_cpu_worker, [(workload, 7 + i, seconds, warm_s) for i in range(procs)])
     dec = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
-    return {"value": dec / wall, "unit": "decisions/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} spawn processes x {seconds:.0f}s of config-2 episodes (J=50, N=10), one env per "
-                      "process, RandomScheduler(seed) — the CPU oracle restatement (real CPython set/dict/heapq, "
-                      "numpy Generator), mirroring trainers/rollout_worker.py"}
+    host = os.cpu_count() or procs
+    value = dec / wall
+    wl = WORKLOADS[workload]
+    return {"value": value, "unit": "decisions/s", "cores": procs, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": host, "usable_cpus": usable_cpus(),
+            "per_core": value / procs, "projected_host": value / procs * host,
+            "episodes_finished": int(sum(r[2] for r in res)), "seconds": wall,
+            "sample": f"{procs} spawn processes (one per usable CPU of this job) x {seconds:.0f} s after a "
+                      f"1-episode warm-up, {workload} workload (J={wl['cfg']['job_arrival_cap']}, "
+                      f"N={wl['cfg']['num_executors']}, {wl['policy']} policy), one env per process: the CPU "
+                      "oracle restatement (real CPython set/dict/heapq, numpy Generator) in the "
+                      "trainers/rollout_worker.py harness shape; projected_host = per_core x host_cpus "
+                      "(an upper bound for the whole host)"}
 
 
+# ------------------------------------------------------------------------------------------------ PMC lookup
 def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisions_per_launch: float):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*/pmc_summary*.json,
     made by scripts/pmc_profile.sh + scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
-    separate passes), scaled from bytes/decision to this launch. None if no matching summary."""
+    separate passes), scaled from bytes/decision to this launch; plus the summary's issue counters per decision
+    when present. (None, None, None) if no summary matches the config."""
     import glob
 
     best = None
@@ -105,27 +236,24 @@ def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisi
         spl = cfg.get("steps_per_launch", k.get("steps") if mode == "rollout" else 1)
         if (cfg.get("mode") == mode and cfg.get("envs_per_gpu") == envs and spl == steps_per_launch
                 and "hbm_bytes_per_decision" in k):
-            best = (path, k["hbm_bytes_per_decision"])
+            best = (path, k)
     if best is None:
-        return None, None
-    return best[1] * decisions_per_launch, os.path.relpath(best[0], REPO)
+        return None, None, None
+    return best[1]["hbm_bytes_per_decision"] * decisions_per_launch, os.path.relpath(best[0], REPO), best[1]
 
 
-def run_ppo(args):
-    """BASELINE configs[4]: whole PPO iterations (GPU rollouts to episode end with the Decima GNN, returns,
-    baselines, PPO epochs) of config/decima_tpch.yaml; one replica per GPU, gradients averaged over RCCL.
+# ------------------------------------------------------------------------------------------------ PPO
+def run_ppo(args, rank, world, local, dev):
+    """BASELINE configs[4]: whole PPO iterations (GPU rollouts with the Decima GNN, returns, baselines, PPO
+    epochs) of config/decima_tpch.yaml; num_sequences x num_rollouts rows split over the ranks, trajectories
+    gathered to one learner (rank 0) over RCCL, parameters broadcast back (trainer.py:85-162).
     `--steps` = timed iterations, `--warmup` = untimed ones; value = rollout decisions / iteration time."""
     import torch
     import torch.distributed as dist
 
-    from spark_sched_sim.distributed import rank_world, reduce_timing
+    from spark_sched_sim.distributed import reduce_timing
     from spark_sched_sim.trainers import DECIMA_TPCH, PPO
 
-    rank, world, local = rank_world()
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    dev = torch.device(f"cuda:{local}")
     cfg = {k: dict(v) for k, v in DECIMA_TPCH.items()}
     if args.ppo_time_limit:
         cfg["env"]["mean_time_limit"] = args.ppo_time_limit
@@ -138,6 +266,7 @@ def run_ppo(args):
     t0 = time.perf_counter()
     dec = 0
     phases = {"collect_s": 0.0, "learn_s": 0.0}
+    learn = None
     for _ in range(args.steps):
         ta = time.perf_counter()
         buf = ppo.collect()
@@ -155,23 +284,25 @@ def run_ppo(args):
     elapsed = time.perf_counter() - t0
     stats = reduce_timing(torch.tensor([elapsed, float(dec)], dtype=torch.float64, device=dev), world)
     elapsed, dec = stats.tolist()
+    line = None
     if rank == 0:
         B = ppo.num_sequences * ppo.num_rollouts
-        print(json.dumps({
+        line = {
             "metric": "scheduling decisions/sec (env steps/s)", "value": dec / elapsed, "unit": "decisions/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 (GNN) + f64/i32 (sim)",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32 (GNN) + f64/i32 (sim)",
             "data": "synthetic TPC-H-format dataset (seeded generator), Decima GNN random init",
-            "config": {"workload": WORKLOADS["ppo"]["desc"].format(B=B), "envs_per_gpu": B,
+            "config": {"workload": WORKLOADS["ppo"]["desc"].format(B=B), "rows_global": B,
                        "mean_time_limit": cfg["env"]["mean_time_limit"], "mode": "ppo",
-                       "parallelism": f"data-parallel x{world}"},
+                       "parallelism": f"rows split over {world} ranks, one learner"},
             "decisions": int(dec), "seconds_per_iteration": elapsed / args.steps,
             "phase_seconds_rank0": phases, "last_learning_stats": learn,
-            "roofline": None, "cpu_baseline": None}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+            "roofline": None, "cpu_baseline": None}
+    return line
 
 
+# ------------------------------------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -180,12 +311,12 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="tpch")
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (0 = the workload's)")
     ap.add_argument("--mode", choices=["rollout", "step"], default="rollout")
-    ap.add_argument("--chunk", type=int, default=0,
-                    help="rollout mode: steps per fused launch (0 = --steps). Warmup runs in launches of the same "
-                         "length (>= --warmup steps in total), so every k_rollout launch is alike and the rocprof "
-                         "per-launch average is the timed launches' duration")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--chunk", type=int, default=0, help="rollout mode: timed steps per fused launch (0 = --steps)")
+    ap.add_argument("--preroll", type=int, default=-1,
+                    help="pre-roll bound (env i takes U[0, preroll) decisions before warm-up; -1 = the workload's, "
+                         "0 = none)")
+    ap.add_argument("--cpu-seconds", type=float, default=60.0)
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = every usable CPU of this job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--torch-policy", action="store_true",
@@ -195,12 +326,15 @@ def main():
     ap.add_argument("--lockstep", action="store_true",
                     help="rollout mode: every env takes exactly `chunk` decisions per launch (ssim_rollout_ex) "
                          "instead of sharing a budget of envs x chunk decisions (ssim_rollout_budget)")
-    ap.add_argument("--compare-lockstep", action="store_true",
-                    help="rollout mode: after the timed region, time one lockstep launch of the same length "
-                         "(off by default so a rocprof of the default run sees only warm-up + timed launches)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="rollout mode: leave finished envs idle instead of resetting them on the device")
+    ap.add_argument("--engine", choices=["hip", "host"], default="hip",
+                    help="host = the TEST-ONLY CPU build of the engine (tests/hostsim) over gloo, to exercise the "
+                         "launcher and the rank plumbing in the CPU test suite; never a measurement")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import numpy as np
     import torch
@@ -209,36 +343,69 @@ def main():
     from spark_sched_sim import _abi
     from spark_sched_sim.data_samplers.synthetic_tpch import generate
     from spark_sched_sim.distributed import gather_env_stats, rank_world, reduce_timing, shard_seeds
-    from spark_sched_sim.engine import DeviceEngine
 
+    host = args.engine == "host"
     rank, world, local = rank_world()
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    dev = torch.device(f"cuda:{local}")
+        if host:
+            dist.init_process_group("gloo", init_method="env://")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cpu") if host else torch.device(f"cuda:{local}")
+
+    def sync():
+        if not host:
+            torch.cuda.synchronize(dev)
 
     if args.workload == "ppo":
-        return run_ppo(args)
+        line = run_ppo(args, rank, world, local, dev)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     wl = WORKLOADS[args.workload]
     cfg = wl["cfg"]
     B, K, W = args.envs or wl["envs"], args.steps, args.warmup
-    if args.workload == "decima":
-        args.mode = "decima"
-    eng = DeviceEngine(cfg, B, generate(0), device=dev)
+    mode = "decima" if args.workload == "decima" else args.mode
+    if host:
+        sys.path.insert(0, os.path.join(REPO, "tests", "hostsim"))
+        from driver import HostEngine  # TEST-ONLY host build (see --engine)
+
+        eng = HostEngine(cfg, B, generate(0))
+        args.lockstep = True  # the host build has no shared-budget launch
+    else:
+        from spark_sched_sim.engine import DeviceEngine
+
+        eng = DeviceEngine(cfg, B, generate(0), device=dev)
     seeds = shard_seeds(rank, B, args.seed)
     limits = None
     if wl["mean_time_limit"]:  # StochasticTimeLimit (wrappers/stochastic_time_limit.py:5-31), per env
         from spark_sched_sim.wrappers import StochasticTimeLimitSampler
 
         smp = StochasticTimeLimitSampler(wl["mean_time_limit"], B, seed=42)
-        limits = torch.tensor([smp.sample(i, int(seeds[i])) for i in range(B)], dtype=torch.float64, device=dev)
-    eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=None if limits is None else limits.cpu().numpy())
+        limits = np.array([smp.sample(i, int(seeds[i])) for i in range(B)], dtype=np.float64)
+    eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=limits)
+    if limits is not None and not host:
+        limits = torch.tensor(limits, dtype=torch.float64, device=dev)
     kind = _abi.SSIM_POLICY_RANDOM
-    stream = torch.cuda.current_stream(dev)
-
-    chunk = args.chunk if args.chunk > 0 else K
+    stream = None if host else torch.cuda.current_stream(dev)
     flags = 0 if args.no_autoreset else _abi.SSIM_ROLLOUT_AUTORESET
-    if args.mode == "decima":
+
+    # 2. pre-roll: spread the batch over the phases of its episodes (seeded per rank)
+    preroll = wl["preroll"] if args.preroll < 0 else args.preroll
+    pre_steps = np.zeros(B, dtype=np.int32)
+    if preroll > 0 and mode != "step":
+        pre_steps = np.random.default_rng([args.seed, rank, 7]).integers(0, preroll, B).astype(np.int32)
+        eng.rollout_steps(kind, 4321, pre_steps, int(pre_steps.max()) + 1, flags=_abi.SSIM_ROLLOUT_AUTORESET,
+                          time_limits=limits)
+    elif preroll > 0:  # step mode: the same spread through the fused launch, then per-step launches
+        pre_steps = np.random.default_rng([args.seed, rank, 7]).integers(0, preroll, B).astype(np.int32)
+        eng.rollout_steps(kind, 4321, pre_steps, int(pre_steps.max()) + 1, flags=0, time_limits=limits)
+
+    if mode == "decima":
         from spark_sched_sim.schedulers.decima import DecimaScheduler, build_batch
 
         torch.manual_seed(args.seed)
@@ -246,104 +413,108 @@ def main():
         gen = torch.Generator(device=dev).manual_seed(args.seed)
         cnt = eng.views["counts"]
         packed = pol.packed_params(dev)  # fixed weights during rollouts: packed once, like RolloutCollector
+        overflow_total = torch.zeros((), dtype=torch.int64, device=dev)
 
-    def chunks(n):
-        return [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
+    def rollout_launch(c):
+        if args.lockstep:
+            eng.rollout(kind, 1234, c, flags=flags, time_limits=limits)
+        else:  # the same B x c decisions, claimed by whichever env is ready (no tail)
+            eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=flags, time_limits=limits)
 
-    def run(n, events=None):
-        if args.mode == "rollout":
-            for k, c in enumerate(chunks(n)):
+    def run(n, events=None, chunk=None):
+        """n steps; `events` (list of HIP event pairs) brackets each kernel launch on the launch stream."""
+        if n <= 0:
+            return
+        if mode == "rollout":
+            chunk = chunk or n
+            sizes = [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
+            for c in sizes:
                 if events is not None:
-                    events[2 * k].record(stream)
-                if args.lockstep:
-                    eng.rollout(kind, 1234, c, flags=flags, time_limits=limits)
-                else:  # the same B x c decisions, claimed by whichever env is ready (no tail)
-                    eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=flags, time_limits=limits)
+                    e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    e[0].record(stream)
+                rollout_launch(c)
                 if events is not None:
-                    events[2 * k + 1].record(stream)
-        elif args.mode == "decima":
-            for k in range(n):
+                    e[1].record(stream)
+                    events.append(e)
+            return
+        for k in range(n):
+            if mode == "decima":
                 if args.torch_policy:  # the batched PyTorch module (~150 launches per decision)
                     act = pol.schedule(build_batch(eng.views, eng.decima_features()), generator=gen)
                 else:  # one fused HIP launch (ssim_decima_policy)
                     run.counter += 1
                     act = pol.schedule_fused(eng, eng.decima_features(), seed=args.seed, counter=run.counter,
                                              params=packed)
-                if events is not None:
-                    events[2 * k].record(stream)
-                eng.step(act["stage_idx"], act["num_exec"])
-                if events is not None:
-                    events[2 * k + 1].record(stream)
-                done = ((cnt[:, _abi.OC_TERMINATED] != 0) | (cnt[:, _abi.OC_TRUNCATED] != 0)).to(torch.uint8)
-                eng.reset_sampled(done, time_limits=limits)  # finished episodes: reset(seed=None) on device
-        else:
-            for k in range(n):
+                    overflow_total.add_(act["overflow"].sum().to(torch.int64))
+                si, ne = act["stage_idx"], act["num_exec"]
+            else:
                 si, ne = eng.policy(kind, 1234, run.counter)
                 run.counter += 1
-                if events is not None:
-                    events[2 * k].record(stream)
-                eng.step(si, ne)
-                if events is not None:
-                    events[2 * k + 1].record(stream)
+            if events is not None:
+                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                e[0].record(stream)
+            eng.step(si, ne)
+            if events is not None:
+                e[1].record(stream)
+                events.append(e)
+            if mode == "decima":
+                done = ((cnt[:, _abi.OC_TERMINATED] != 0) | (cnt[:, _abi.OC_TRUNCATED] != 0)).to(torch.uint8)
+                eng.reset_sampled(done, time_limits=limits)  # finished episodes: reset(seed=None) on device
     run.counter = 0
 
-    if args.mode == "rollout":
-        W = -(-W // chunk) * chunk if W > 0 else 0  # whole launches of `chunk` steps
+    # 3. warm-up: exactly W steps
     run(W)
-    torch.cuda.synchronize(dev)
-    counts0 = eng.views["counts"].cpu().numpy().copy()
-    acc0 = eng.views["acc"].cpu().numpy().copy()
-    launches = len(chunks(K)) if args.mode == "rollout" else K
-    n_ev = 2 * launches
-    events = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+    sync()
+    acc0 = np.array(eng.to_numpy(eng.views["acc"]), dtype=np.int64).copy()
+    events = None if host else []
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
-    run(K, events)
-    torch.cuda.synchronize(dev)
+    run(K, events, args.chunk or K)  # 4. timed: exactly K steps
+    sync()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    counts1 = eng.views["counts"].cpu().numpy()
-    acc1 = eng.views["acc"].cpu().numpy()
-    lockstep = None
-    if args.mode == "rollout" and not args.lockstep and args.compare_lockstep:
-        # off the clock: one lockstep launch of the same length (every env exactly `chunk` decisions) for
-        # comparison -- its time is set by the env whose `chunk` decisions cost the most
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        a0 = eng.views["acc"].cpu().numpy().copy()
-        ev[0].record(stream)
-        eng.rollout(kind, 1234, chunk, flags=flags, time_limits=limits)
-        ev[1].record(stream)
-        torch.cuda.synchronize(dev)
-        ld = float((eng.views["acc"].cpu().numpy() - a0).sum(axis=0)[_abi.ACC_DECISIONS])
-        lockstep = {"decisions": int(ld), "kernel_ms": ev[0].elapsed_time(ev[1]),
-                    "decisions_per_s": ld / (ev[0].elapsed_time(ev[1]) / 1e3)}
+    v = eng.host_views()
+    counts1 = np.array(v["counts"])
+    acc1 = np.array(v["acc"], dtype=np.int64)
     errs = int(np.count_nonzero(counts1[:, _abi.OC_ERR] & _abi.SSIM_ERR_STICKY))
     d_acc = (acc1 - acc0).sum(axis=0).astype(np.float64)  # S_act, E_act, J_act, events, decisions, episodes
-    decisions = int(d_acc[_abi.ACC_DECISIONS])  # over all episodes (auto-reset restarts the per-episode count)
-    terminated = int(counts1[:, _abi.OC_TERMINATED].sum())
-    episodes_done = int(d_acc[_abi.ACC_EPISODES])
+    decisions = float(d_acc[_abi.ACC_DECISIONS])  # over all episodes (auto-reset restarts the per-episode count)
+    episodes_done = float(d_acc[_abi.ACC_EPISODES])
     # SURVEY.md §8d: B_dec = 36 S_act + 20 E_act + 16 J_act + 96 K + 40 bytes per decision
     alg_bytes = 36 * d_acc[0] + 20 * d_acc[1] + 16 * d_acc[2] + 96 * d_acc[3] + 40 * decisions
-    kern_ms = sum(events[2 * k].elapsed_time(events[2 * k + 1]) for k in range(launches))
+    launches = len(events) if events is not None else 0
+    kern_ms = sum(a.elapsed_time(b) for a, b in events) if events else 0.0
     elapsed = t1 - t0
-    stats = torch.tensor([elapsed, float(decisions), alg_bytes, kern_ms, float(errs), float(terminated)],
+    stats = torch.tensor([elapsed, decisions, alg_bytes, kern_ms, float(errs), episodes_done, float(d_acc[3])],
                          dtype=torch.float64, device=dev)
     stats = reduce_timing(stats, world)
-    # episode statistics gather (the only data collective; RCCL all_gather, off the timed path)
     mine = torch.tensor(counts1[:, [_abi.OC_NUM_COMPLETED, _abi.OC_NUM_ARRIVED, _abi.OC_DECISIONS]],
                         dtype=torch.int32, device=dev)
-    gathered = gather_env_stats(mine, world)
-    elapsed, decisions, alg_bytes, kern_ms_sum, errs, terminated = stats.tolist()
-    kern_ms = kern_ms_sum / world
+    gathered = gather_env_stats(mine, world)  # episode statistics gather (off the timed path)
+    elapsed, decisions, alg_bytes, kern_ms_sum, errs, episodes_done, events_sum = stats.tolist()
+    overflow = int(overflow_total.item()) if mode == "decima" and not args.torch_policy else 0
     value = decisions / elapsed
-    achieved = (alg_bytes / world / launches) / (kern_ms / launches / 1e3) / 1e9  # GB/s per GPU, dominant kernel
-    kernel = "k_rollout" if args.mode == "rollout" else "k_step"
-    traffic, traffic_src = pmc_traffic(kernel, args.mode, B, chunk if args.mode == "rollout" else 1,
-                                       decisions / world / launches)
+    line = None
     if rank == 0:
+        kernel = "k_rollout" if mode == "rollout" else "k_step"
+        roofline = None
+        if not host and launches:
+            kern_ms = kern_ms_sum / world
+            achieved = (alg_bytes / world / launches) / (kern_ms / launches / 1e3) / 1e9  # GB/s per GPU
+            traffic, traffic_src, pmc = pmc_traffic(kernel, mode, B, K if mode == "rollout" else 1,
+                                                   decisions / world / launches)
+            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                        "kernel": kernel, "kernel_ms_per_launch": kern_ms / launches,
+                        "alg_bytes_per_launch": alg_bytes / world / launches}
+            if pmc is not None and "issue" in pmc:
+                # the bound that binds: instruction issue of one wave per SIMD (DESIGN.md §4)
+                iss = dict(pmc["issue"])
+                iss["decisions_per_s_per_simd"] = decisions / elapsed / world / pmc["issue"].get("simds", 1024)
+                roofline["issue"] = iss
         line = {
             "metric": "scheduling decisions/sec (env steps/s)",
             "value": value,
@@ -357,39 +528,40 @@ def main():
             "vs_baseline": None,
             "dtype": "f64+i32",
             "data": "synthetic TPC-H-format dataset (seeded generator), " + (
-                "Decima GNN policy, random-init weights" if args.mode == "decima" else
-                "random valid actions (device RNG)"),
+                "Decima GNN policy, random-init weights" if mode == "decima" else "random valid actions (device RNG)"),
             "config": {"workload": wl["desc"].format(B=B), "envs_per_gpu": B,
                        "jobs": cfg["job_arrival_cap"], "executors": cfg["num_executors"],
-                       "mean_time_limit": wl["mean_time_limit"], "mode": args.mode,
-                       "policy": ("torch" if args.torch_policy else "fused HIP kernel") if args.mode == "decima"
+                       "mean_time_limit": wl["mean_time_limit"], "mode": mode,
+                       "policy": ("torch" if args.torch_policy else "fused HIP kernel") if mode == "decima"
                        else "device random",
-                       "steps_per_launch": chunk if args.mode == "rollout" else 1,
+                       "steps_per_launch": (args.chunk or K) if mode == "rollout" else 1,
                        "work_sharing": ("lockstep" if args.lockstep else "shared budget of envs x steps "
-                                        "decisions per launch") if args.mode == "rollout" else None,
-                       "autoreset": bool(args.mode != "step" and (flags or args.mode == "decima")),
+                                        "decisions per launch") if mode == "rollout" else None,
+                       "preroll": {"bound": preroll, "mean_decisions": float(pre_steps.mean())},
+                       "autoreset": bool(mode != "step" and (flags or mode == "decima")),
                        "parallelism": f"env-sharded x{world}"},
             "decisions": int(decisions),
-            "terminated_envs": int(terminated),
-            "episodes_finished": episodes_done,
+            "episodes_finished": int(episodes_done),
+            "events_per_decision": events_sum / max(decisions, 1.0),
+            "terminated_envs": int((counts1[:, _abi.OC_TERMINATED] != 0).sum()),
             "frozen_envs": int(errs),
             "jobs_completed": int(gathered[:, 0].sum().item()),
             "jobs_arrived": int(gathered[:, 1].sum().item()),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": kernel,
-                         "kernel_ms_per_launch": kern_ms / launches,
-                         "alg_bytes_per_launch": alg_bytes / world / launches},
+            "roofline": roofline,
             "cpu_baseline": None,
         }
-        if lockstep is not None:
-            line["lockstep_1gpu"] = lockstep
-        if not args.no_cpu_baseline and world == 1 and args.workload == "tpch":
-            procs = args.cpu_procs or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, procs)
+        if mode == "decima":
+            line["policy_overflow_envs"] = overflow
+        if host:
+            line["engine"] = "hostsim (TEST-ONLY CPU build; not a measurement)"
+        if not args.no_cpu_baseline and world == 1 and not host and args.workload in ("tpch", "large", "decima"):
+            procs = args.cpu_procs or usable_cpus()
+            line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, procs)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if mode == "decima" and overflow:
+        raise SystemExit(f"fused Decima policy skipped {overflow} env-steps (LDS node cap overflow)")
 
 
 if __name__ == "__main__":

@@ -95,9 +95,15 @@ template <bool kRes, int kN, int kJ, int kS>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_ROLLOUT_WAVES))) void k_rollout(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                 int kind, uint64_t seed, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
-                                                int32_t* action_log, uint64_t* prof_out, int64_t budget) {
+                                                int32_t* action_log, uint64_t* prof_out, int64_t budget,
+                                                const int32_t* __restrict__ env_steps) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
+  if (env_steps != nullptr) {  // per-env decision counts (ssim_rollout_steps), capped by num_steps
+    const int n = env_steps[eid];
+    num_steps = n < num_steps ? n : num_steps;
+    if (num_steps <= 0) return;
+  }
   const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   if (env_idle(P, state, eid) && action_log == nullptr && !autoreset) return;
   Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
@@ -200,7 +206,7 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
 // dataset), else the generic ones.
 using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
 using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int, const double*, uint8_t*,
-                          int32_t*, uint64_t*, int64_t);
+                          int32_t*, uint64_t*, int64_t, const int32_t*);
 static bool bench_shape(const Params& p) {
   return p.L.num_executors == 10 && p.L.job_cap == 50 && p.L.stage_cap == 900;
 }
@@ -330,7 +336,8 @@ extern "C" int ssim_policy(ssim_handle* h, int32_t kind, uint64_t seed, uint64_t
 }
 
 static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int64_t budget,
-                          int32_t flags, const double* time_limits, int32_t* action_log, void* stream) {
+                          int32_t flags, const double* time_limits, int32_t* action_log, void* stream,
+                          const int32_t* env_steps = nullptr) {
   if (h == nullptr || num_steps < 0 || budget < 0) return set_err(SSIM_E_ARG, "ssim_rollout: bad argument");
   if (kind != SSIM_POLICY_FAIR && kind != SSIM_POLICY_FIFO && kind != SSIM_POLICY_RANDOM)
     return set_err(SSIM_E_ARG, "ssim_rollout: unknown policy %d", kind);
@@ -344,7 +351,7 @@ static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t n
   }
   hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, flags, time_limits, h->reset, action_log,
-                     (uint64_t*)nullptr, budget);
+                     (uint64_t*)nullptr, budget, env_steps);
   return hip_check(hipGetLastError(), "k_rollout launch");
 }
 
@@ -358,6 +365,13 @@ extern "C" int ssim_rollout_budget(ssim_handle* h, int32_t kind, uint64_t seed, 
                                    int32_t* action_log, void* stream) {
   if (total_decisions <= 0) return set_err(SSIM_E_ARG, "ssim_rollout_budget: total_decisions must be > 0");
   return rollout_launch(h, kind, seed, max_steps, total_decisions, flags, time_limits, action_log, stream);
+}
+
+extern "C" int ssim_rollout_steps(ssim_handle* h, int32_t kind, uint64_t seed, const int32_t* env_steps,
+                                  int32_t max_steps, int32_t flags, const double* time_limits, int32_t* action_log,
+                                  void* stream) {
+  if (env_steps == nullptr) return set_err(SSIM_E_ARG, "ssim_rollout_steps: null env_steps");
+  return rollout_launch(h, kind, seed, max_steps, 0, flags, time_limits, action_log, stream, env_steps);
 }
 
 extern "C" int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t* action_log,
@@ -383,7 +397,7 @@ extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed
   const ssim_layout& L = h->params.L;
   hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, 0, (const double*)nullptr, h->reset,
-                     (int32_t*)nullptr, prof_out, (int64_t)0);
+                     (int32_t*)nullptr, prof_out, (int64_t)0, (const int32_t*)nullptr);
   return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
 }
 #endif
@@ -432,12 +446,19 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
   if (lds > kDecimaPolicyLdsMax)
     return set_err(SSIM_E_ARG, "ssim_decima_policy: node_cap %d needs %lld B of LDS (max %lld)", node_cap,
                    (long long)lds, (long long)kDecimaPolicyLdsMax);
-  static int64_t configured = 0;
-  if (lds > 64 * 1024 && lds > configured) {
-    int rc = hip_check(hipFuncSetAttribute((const void*)k_decima_policy, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds), "k_decima_policy LDS attribute");
+  if (lds > 64 * 1024) {
+    // hipFuncSetAttribute is per-device state: remember the raised limit per device (a process may drive
+    // several GPUs); the cache is a fast path only, a race at worst repeats the (idempotent) call
+    static int64_t configured[64] = {0};
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
     if (rc != SSIM_OK) return rc;
-    configured = lds;
+    if (dev < 0 || dev >= 64 || lds > configured[dev]) {
+      rc = hip_check(hipFuncSetAttribute((const void*)k_decima_policy, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds), "k_decima_policy LDS attribute");
+      if (rc != SSIM_OK) return rc;
+      if (dev >= 0 && dev < 64) configured[dev] = lds;
+    }
   }
   DecimaPolicyOut o{stage_idx, num_exec, job_idx, exec_idx, lgprob, stage_scores, exec_scores};
   hipLaunchKernelGGL(k_decima_policy, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream, dparams(h),

@@ -322,6 +322,23 @@ class DeviceEngine:
             self.handle, kind, seed, max_steps, total_decisions, flags, None if tl is None else tl.data_ptr(), ptr,
             self._stream()), "ssim_rollout_budget")
 
+    def rollout_steps(self, kind: int, seed: int, env_steps, max_steps: int, action_log=None, flags: int = 0,
+                      time_limits=None):
+        """ssim_rollout_steps: env i takes min(env_steps[i], max_steps) fused policy+step decisions in one
+        launch (env_steps: int32 [num_envs], host or device)."""
+        t = self.torch
+        st = t.as_tensor(np.asarray(env_steps, dtype=np.int32).reshape(self.num_envs), device=self.device) \
+            if not isinstance(env_steps, t.Tensor) else env_steps.to(device=self.device, dtype=t.int32).contiguous()
+        ptr = action_log.data_ptr() if action_log is not None else None
+        tl = None
+        if time_limits is not None:
+            tl = t.as_tensor(np.asarray(time_limits, dtype=np.float64).reshape(self.num_envs),
+                             device=self.device) if not hasattr(time_limits, "data_ptr") else time_limits
+        self._keep_tl = (st, tl)
+        self._native.check(self._native.lib().ssim_rollout_steps(
+            self.handle, kind, seed, st.data_ptr(), max_steps, flags, None if tl is None else tl.data_ptr(), ptr,
+            self._stream()), "ssim_rollout_steps")
+
     def host_views(self) -> dict:
         return arena_views(self.obs.cpu().numpy(), self.layout)
 

@@ -17,9 +17,40 @@ import numpy as np
 
 from . import _abi
 from .engine import DeviceEngine, decode_trace, executor_histories, obs_dict
-from .spaces import ActionSpace
+from .spaces import action_space, observation_space
 
 NUM_NODE_FEATURES = 3
+
+try:  # a gymnasium.Env subclass when gymnasium is importable (gym.make / wrappers then work unchanged)
+    from gymnasium import Env as _EnvBase  # type: ignore
+except Exception:  # noqa: BLE001 - gymnasium is not installed in this image
+
+    class _EnvBase:  # the attributes of gymnasium.Env the reference's callers touch
+        metadata: dict = {}
+        render_mode = None
+        spec = None
+
+        @property
+        def unwrapped(self):
+            return self
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *exc):
+            self.close()
+            return False
+
+
+def resolve_dataset(env_cfg: dict, dataset=None):
+    """The tables the device samples from: an explicit `dataset` (raw {(q, size): (adj, tds)} dict or
+    PackedDataset) wins; otherwise the config's data sampler plugin (make_data_sampler, defaulting to
+    TPCHDataSampler over data/tpch, spark_sched_sim.py:54 / data_samplers/__init__.py:9-15)."""
+    if dataset is not None:
+        return dataset
+    from .data_samplers import make_data_sampler
+
+    return make_data_sampler(env_cfg).packed(env_cfg["num_executors"])
 
 
 def _raise_for(err: int, action) -> None:
@@ -37,8 +68,8 @@ def _raise_for(err: int, action) -> None:
         raise RuntimeError(f"device capacity/reset error {err:#x}")
 
 
-class SparkSchedSimEnv:
-    """A Gymnasium-style env that simulates DAG job scheduling in Spark, stepped on the GPU."""
+class SparkSchedSimEnv(_EnvBase):
+    """A Gymnasium environment that simulates DAG job scheduling in Spark, stepped on the GPU."""
 
     metadata = {"render_modes": ["human"], "render_fps": 30}
 
@@ -51,19 +82,14 @@ class SparkSchedSimEnv:
         self.render_mode = env_cfg.get("render_mode")
         if self.render_mode == "human":
             raise ValueError("pygame is unavailable")  # rendering is out of scope (no renderer is built)
-        sampler = env_cfg.get("data_sampler_cls", "TPCHDataSampler")
-        if sampler != "TPCHDataSampler":
-            raise AssertionError(f"'{sampler}' is not a valid data sampler.")
-        if dataset is None:
-            from .data_samplers.synthetic_tpch import generate
-
-            dataset = generate(0)
+        dataset = resolve_dataset(env_cfg, dataset)
         # history_cap > 0 records the per-episode event trace (that many records) for render_data()
         self.history_cap = int(history_cap)
         factory = _engine_factory or (lambda cfg, ds: DeviceEngine(cfg, 1, ds, device=device, job_cap=job_cap,
                                                                    trace_cap=self.history_cap))
         self._eng = factory(dict(env_cfg), dataset)
-        self.action_space = ActionSpace(self.num_executors)
+        self.action_space = action_space(self.num_executors)
+        self.observation_space = observation_space(self.num_executors)
         self.job_duration_buff: deque = deque(maxlen=200)
         self.wall_time = 0.0
         self._obs = None
@@ -80,6 +106,7 @@ class SparkSchedSimEnv:
         if err:
             _raise_for(err, {"stage_idx": None})
         self.job_arrival_cap = self._eng.sampler.arrival_cap[0]
+        self.observation_space["source_job_idx"].n = self.job_arrival_cap + 1  # :157
         return self._observe(v), self.info
 
     def step(self, action: dict):
@@ -121,7 +148,12 @@ class SparkSchedSimEnv:
 
     @property
     def avg_job_duration(self) -> float:
-        return np.mean(list(self.job_duration_buff) + self._episode_durations()).item() * 1e-3
+        """Mean of the last 200 job durations over all episodes (spark_sched_sim.py:83,243-245,697: one
+        deque(maxlen=200) that survives resets). The current episode's completions are appended in completion
+        order to the finished episodes' buffer, then the window is cut to 200."""
+        window = deque(self.job_duration_buff, maxlen=200)
+        window.extend(self._episode_durations())
+        return np.mean(window).item() * 1e-3
 
     def job_times(self):
         """(t_arrival, t_completed, state) numpy arrays of this episode's jobs."""
@@ -172,7 +204,9 @@ class SparkSchedSimEnv:
     def _observe(self, v):
         obs = obs_dict(v, 0)
         self.wall_time = float(v["wall_time"][0])
-        self.action_space["stage_idx"].n = obs["dag_batch"].nodes.shape[0] + 1
+        n = obs["dag_batch"].nodes.shape[0] + 1
+        self.action_space["stage_idx"].n = n  # :403-404
+        self.observation_space["dag_ptr"].feature_space.n = n
         return obs
 
     def _episode_durations(self):

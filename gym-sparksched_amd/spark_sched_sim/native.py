@@ -37,6 +37,7 @@ def lib() -> ct.CDLL:
     L.ssim_rollout.argtypes = [vp, i32, u64, i32, vp, vp]
     L.ssim_rollout_ex.argtypes = [vp, i32, u64, i32, i32, vp, vp, vp]
     L.ssim_rollout_budget.argtypes = [vp, i32, u64, i32, ct.c_int64, i32, vp, vp, vp]
+    L.ssim_rollout_steps.argtypes = [vp, i32, u64, vp, i32, i32, vp, vp, vp]
     L.ssim_reset_sampled.argtypes = [vp, vp, vp, vp, vp]
     L.ssim_decima_policy.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                      vp]
@@ -44,7 +45,8 @@ def lib() -> ct.CDLL:
     L.ssim_decima_features.argtypes = [vp, ct.c_float, ct.c_float, vp, vp, vp, vp, vp]
     L.ssim_last_error.restype = ct.c_char_p
     for name in ("ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
-                 "ssim_rollout", "ssim_job_times", "ssim_decima_features"):
+                 "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
+                 "ssim_job_times", "ssim_decima_features", "ssim_decima_policy"):
         getattr(L, name).restype = ct.c_int
     _lib = L
     return L
@@ -56,5 +58,6 @@ def check(rc: int, what: str) -> None:
 
 
 EXPORTED_SYMBOLS = ["ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
-                    "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_reset_sampled", "ssim_job_times",
+                    "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
+                    "ssim_job_times",
                     "ssim_decima_features", "ssim_decima_policy", "ssim_last_error"]

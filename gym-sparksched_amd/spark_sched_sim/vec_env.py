@@ -16,14 +16,23 @@ from .engine import DeviceEngine
 from .wrappers import StochasticTimeLimitSampler
 
 
-class SparkSchedSimVecEnv:
-    def __init__(self, env_cfg: dict, num_envs: int, dataset=None, device="cuda", job_cap=None,
-                 mean_time_limit: float | None = None, time_limit_seed: int = 42, trace_cap: int = 0):
-        if dataset is None:
-            from .data_samplers.synthetic_tpch import generate
+DEVICE_RESET_MIN_ENVS = 1024  # reset() samples job sequences in the reset kernel from this batch size up
 
-            dataset = generate(0)
+
+class SparkSchedSimVecEnv:
+    """`device_reset`: None = job sequences drawn by the reset kernel (ssim_reset_sampled) when num_envs >=
+    DEVICE_RESET_MIN_ENVS, else on the host with numpy (ssim_reset); True / False force one path. Both give
+    the same episodes bit for bit (tests/cases.py case_sampled_reset)."""
+
+    def __init__(self, env_cfg: dict, num_envs: int, dataset=None, device="cuda", job_cap=None,
+                 mean_time_limit: float | None = None, time_limit_seed: int = 42, trace_cap: int = 0,
+                 device_reset: bool | None = None):
+        from .env import resolve_dataset
+
+        dataset = resolve_dataset(env_cfg, dataset)
         self.num_envs = num_envs
+        self.device_reset = (num_envs >= DEVICE_RESET_MIN_ENVS) if device_reset is None else bool(device_reset)
+        self._ever_reset = np.zeros(num_envs, dtype=bool)
         self.num_executors = env_cfg["num_executors"]
         self.engine = DeviceEngine(env_cfg, num_envs, dataset, device=device, job_cap=job_cap, trace_cap=trace_cap)
         self.device = self.engine.device
@@ -41,13 +50,43 @@ class SparkSchedSimVecEnv:
         }
 
     def reset(self, seed=None, options=None, env_ids=None):
+        """reset(seed, options) of the envs `env_ids` (default all). seed: None (continue each env's stream, or
+        fresh entropy for an env never reset), an int base (env i gets base + i) or one seed per listed env.
+        options: {"time_limit": t} for all, or a list of per-env option dicts."""
         ids = list(range(self.num_envs)) if env_ids is None else list(env_ids)
+        seeds = None if seed is None else ([seed + i for i in ids] if np.isscalar(seed) else list(seed))
         if self._limits is not None:
-            seeds = None if seed is None else ([seed + i for i in ids] if np.isscalar(seed) else list(seed))
             options = [{"time_limit": self._limits.sample(i, None if seeds is None else seeds[k])}
                        for k, i in enumerate(ids)]
-        self.engine.reset(seeds=seed, options=options, env_ids=env_ids)
+        if self.device_reset:
+            self._reset_on_device(ids, seeds, options)
+        else:
+            self.engine.reset(seeds=seed, options=options, env_ids=env_ids)
+        self._ever_reset[ids] = True
         return self.obs, self._info()
+
+    def _reset_on_device(self, ids, seeds, options):
+        """One ssim_reset_sampled launch: the reset kernel draws each listed env's job sequence from its
+        Generator stream (tpch.py:54-73) and resets it; the other envs are left as they are."""
+        from .data_samplers.job_sequence import time_limit_or_inf
+
+        B = self.num_envs
+        mode = np.full(B, _abi.SSIM_RESET_SKIP, dtype=np.uint8)
+        sd = np.zeros(B, dtype=np.uint64)
+        lim = np.full(B, np.inf)
+        fresh = np.random.SeedSequence().generate_state(len(ids), dtype=np.uint64) if seeds is None else None
+        for k, i in enumerate(ids):
+            if seeds is not None:
+                mode[i], sd[i] = _abi.SSIM_RESET_SEED, np.uint64(int(seeds[k]) & 0xFFFFFFFFFFFFFFFF)
+            elif self._ever_reset[i]:
+                mode[i] = _abi.SSIM_RESET_CONTINUE
+            else:  # gymnasium seeds a never-reset env from OS entropy
+                mode[i], sd[i] = _abi.SSIM_RESET_SEED, fresh[k]
+            opt = options[k] if isinstance(options, (list, tuple)) else options
+            lim[i] = time_limit_or_inf(opt)
+        if np.isinf(lim[mode != _abi.SSIM_RESET_SKIP]).any() and not self.engine.cfg.job_arrival_cap:
+            raise ValueError("must either have a limit on job arrivals or time.")
+        self.engine.reset_sampled(mode, seeds=sd, time_limits=lim)
 
     def step(self, stage_idx, num_exec):
         self.engine.step(stage_idx, num_exec)

@@ -198,6 +198,12 @@ int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_ste
 int ssim_rollout_budget(ssim_handle* h, int32_t kind, uint64_t seed, int32_t max_steps, int64_t total_decisions,
                         int32_t flags, const double* time_limits, int32_t* action_log, void* stream);
 
+/* ssim_rollout_ex with a per-env decision count: env i takes min(env_steps[i], max_steps) decisions (device int32
+ * [num_envs]); action_log rows as ssim_rollout_ex. Used to spread a batch over the phases of its episodes (a
+ * benchmark's pre-roll) or to give every env its own horizon. */
+int ssim_rollout_steps(ssim_handle* h, int32_t kind, uint64_t seed, const int32_t* env_steps, int32_t max_steps,
+                       int32_t flags, const double* time_limits, int32_t* action_log, void* stream);
+
 /* Per-job results for metrics (spark_sched_sim/metrics.py): t_arrival/t_completed float64 [num_envs][job_cap]
  * and job state int32 [num_envs][job_cap] (0 not arrived, 1 active, 2 completed), any may be NULL. */
 int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32_t* state, void* stream);

@@ -60,6 +60,7 @@ def lib():
         L.hs_decima.argtypes = [vp, ct.c_float, ct.c_float, vp, vp, vp, vp]
         L.hs_reset_sampled.argtypes = [vp, vp, vp, vp]
         L.hs_rollout_ex.argtypes = [vp, ct.c_int, ct.c_uint64, ct.c_int, ct.c_int, vp, vp]
+        L.hs_rollout_steps.argtypes = [vp, ct.c_int, ct.c_uint64, vp, ct.c_int, ct.c_int, vp, vp]
         L.hs_seed_words.argtypes = [ct.c_uint64, vp]
         L.hs_std_exponential.argtypes = [vp, ct.c_int, vp]
         L.hs_log1p.argtypes = [vp, ct.c_int, vp]
@@ -138,6 +139,15 @@ class HostEngine:
                                  ptr)
         assert rc == 0, "hostsim rollout: the hot-block policy view disagreed with the obs-arena view" if rc == -5 \
             else f"hostsim rollout rc={rc}"
+
+    def rollout_steps(self, kind, seed, env_steps, max_steps, action_log=None, flags=0, time_limits=None):
+        st = np.ascontiguousarray(np.asarray(env_steps, dtype=np.int32).reshape(self.num_envs))
+        ptr = action_log.ctypes.data if action_log is not None else None
+        tl = None if time_limits is None else np.ascontiguousarray(np.asarray(time_limits, dtype=np.float64))
+        self._keep_tl = (st, tl)
+        rc = lib().hs_rollout_steps(self.handle, kind, seed, st.ctypes.data, max_steps, flags,
+                                    None if tl is None else tl.ctypes.data, ptr)
+        assert rc == 0, f"hostsim rollout_steps rc={rc}"
 
     def host_views(self):
         return self.views

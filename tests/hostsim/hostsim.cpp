@@ -156,14 +156,23 @@ int hs_rollout(hs_handle* h, int kind, uint64_t seed, int num_steps, int32_t* ac
   return hs_rollout_ex(h, kind, seed, num_steps, 0, nullptr, action_log);
 }
 
+int hs_rollout_steps(hs_handle* h, int kind, uint64_t seed, const int32_t* env_steps, int num_steps, int flags,
+                     const double* limits, int32_t* action_log);
 int hs_rollout_ex(hs_handle* h, int kind, uint64_t seed, int num_steps, int flags, const double* limits,
                   int32_t* action_log) {
+  return hs_rollout_steps(h, kind, seed, nullptr, num_steps, flags, limits, action_log);
+}
+
+// ssim_rollout_steps: env e takes min(env_steps[e], num_steps) decisions (all num_steps when env_steps is null)
+int hs_rollout_steps(hs_handle* h, int kind, uint64_t seed, const int32_t* env_steps, int num_steps, int flags,
+                     const double* limits, int32_t* action_log) {
   const Params* P = h->params;
   const int B = P->L.num_envs;
   for (int e = 0; e < B; ++e) {
     Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
     PolicyView<WaveSerial> v{P->L, h->obs, e};
-    for (int k = 0; k < num_steps; ++k) {
+    const int steps = env_steps != nullptr && env_steps[e] < num_steps ? env_steps[e] : num_steps;
+    for (int k = 0; k < steps; ++k) {
       // the device rollout's policy (picks from the hot block) must equal the obs-arena view's (k_policy)
       s.load_header();
       const StepIn a = sim_policy(s, kind, seed);

@@ -169,3 +169,34 @@ def check_render_history(env, ref):
     assert rd["job_completion_times"] == [ref.jobs[j].t_completed for j in ref.completed_ids]
     assert rd["average_job_duration"] == int(R.avg_job_duration(ref) * 1e-3)
     assert rd["num_jobs_completed"] == len(ref.completed_ids) and rd["wall_time"] == ref.wall_time
+
+
+def test_observation_space_matches_reference_structure(dataset, env_cfg):
+    """spark_sched_sim.py:96-125 (+ the updates at :157 and :403-404): the env's observations are members of
+    its observation_space; source_job_idx.n = jobs + 1 after reset, dag_ptr.feature_space.n = nodes + 1."""
+    env = SparkSchedSimEnv(env_cfg, dataset, _engine_factory=host_factory())
+    sp = env.observation_space
+    assert set(sp.keys()) == {"dag_batch", "dag_ptr", "num_committable_execs", "source_job_idx", "exec_supplies"}
+    assert sp["num_committable_execs"].n == 11 and sp["exec_supplies"].feature_space.n == 20
+    assert sp["dag_batch"].node_space.shape == (3,)
+    obs, _ = env.reset(seed=21)
+    assert sp["source_job_idx"].n == env.job_arrival_cap + 1
+    pol = FairPolicy(10)
+    for k in range(60):
+        assert sp.contains(obs), f"step {k}"
+        assert sp["dag_ptr"].feature_space.n == obs["dag_batch"].nodes.shape[0] + 1
+        assert env.action_space["stage_idx"].n == obs["dag_batch"].nodes.shape[0] + 1
+        obs, *_ = env.step(pol.schedule(obs)[0])
+    bad = dict(obs, num_committable_execs=11)
+    assert not sp.contains(bad)
+
+
+def test_avg_job_duration_window_spans_episodes(dataset, env_cfg):
+    """The duration buffer is one deque(maxlen=200) over all episodes (spark_sched_sim.py:83,243-245,697): with
+    50-job episodes the window is full after 4 episodes and then holds only the last 200 completions."""
+    env = SparkSchedSimEnv(env_cfg, dataset, _engine_factory=host_factory())
+    ref = R.SparkSchedOracle(env_cfg, dataset)
+    for ep, seed in enumerate((3, 4, 5, 6, 7)):
+        run_facade_vs_oracle(env, ref, FairPolicy(10), seed=seed)
+        assert np.isclose(env.avg_job_duration, ref.avg_job_duration, rtol=1e-12), f"episode {ep}"
+    assert len(ref.duration_buff) == 200
