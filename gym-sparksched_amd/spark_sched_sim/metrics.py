@@ -27,3 +27,57 @@ def avg_num_jobs(env) -> float:
 
 def job_duration_percentiles(env):
     return np.percentile(job_durations(env), [25, 50, 75, 100])
+
+
+class RowStats:
+    """rollout_worker.py:122-129 `collect_stats` for every row of a batched engine (a row = one reference worker
+    whose env persists across resets):
+      avg_job_duration  env.avg_job_duration: mean of the last 200 job durations over ALL of the row's episodes
+                        (one deque(maxlen=200), spark_sched_sim.py:83,243-245,697), in seconds;
+      avg_num_jobs      metrics.avg_num_jobs of the current episode (durations of active and completed jobs up
+                        to the wall time, / wall time);
+      num_completed_jobs, num_job_arrivals (completed + active) of the current episode.
+    Call `flush(rows, engine)` before an engine resets `rows` (their finished episode's completions enter the
+    windows); `stats(engine)` -> float64 [B, 4]. Completions enter a window in completion-time order (stable in
+    job id for equal times)."""
+
+    def __init__(self, num_rows: int, cap: int = 200):
+        from collections import deque
+
+        self.windows = [deque(maxlen=cap) for _ in range(num_rows)]
+        self.started = np.zeros(num_rows, dtype=bool)
+
+    @staticmethod
+    def _completed(ta, tc, st, e):
+        done = np.nonzero(st[e] == 2)[0]
+        order = done[np.argsort(tc[e, done], kind="stable")]
+        return (tc[e, order] - ta[e, order]).tolist()
+
+    def flush(self, rows, engine) -> None:
+        rows = [int(r) for r in rows]
+        if not any(self.started[r] for r in rows):
+            self.started[rows] = True
+            return
+        ta, tc, st = (np.asarray(x) for x in engine.job_times_np())
+        for e in rows:
+            if self.started[e]:
+                self.windows[e].extend(self._completed(ta, tc, st, e))
+        self.started[rows] = True
+
+    def stats(self, engine) -> np.ndarray:
+        from collections import deque
+
+        ta, tc, st = (np.asarray(x) for x in engine.job_times_np())
+        wall = np.asarray(engine.host_views()["wall_time"], dtype=np.float64)
+        B = ta.shape[0]
+        out = np.zeros((B, 4))
+        for e in range(B):
+            w = deque(self.windows[e], maxlen=self.windows[e].maxlen)
+            w.extend(self._completed(ta, tc, st, e))
+            out[e, 0] = (np.mean(w) if len(w) else np.nan) * 1e-3
+            arrived = st[e] > 0
+            dur = np.minimum(tc[e, arrived], wall[e]) - ta[e, arrived]
+            out[e, 1] = dur.sum() / wall[e] if wall[e] > 0 else np.nan
+            out[e, 2] = float((st[e] == 2).sum())
+            out[e, 3] = float(arrived.sum())
+        return out

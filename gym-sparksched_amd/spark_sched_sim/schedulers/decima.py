@@ -269,10 +269,39 @@ def masked_softmax_stats(scores: torch.Tensor, mask: torch.Tensor, seg: torch.Te
     return torch.where(mask, probs, torch.zeros_like(probs)), logp
 
 
-def gumbel_pick(logp: torch.Tensor, seg: torch.Tensor, nseg: int, generator=None) -> torch.Tensor:
+def _i64(c: int) -> int:  # a 64-bit constant as the signed value torch int64 arithmetic wraps around
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+def _lsr(x: torch.Tensor, s: int) -> torch.Tensor:  # logical shift right of int64 bit patterns
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def _mix64(x: torch.Tensor) -> torch.Tensor:
+    """splitmix64 (the device policies' counter-based stream, csrc/policy.h) on int64 tensors; torch integer
+    arithmetic wraps modulo 2^64 like the uint64 original."""
+    x = x + _i64(0x9E3779B97F4A7C15)
+    x = (x ^ _lsr(x, 30)) * _i64(0xBF58476D1CE4E5B9)
+    x = (x ^ _lsr(x, 27)) * _i64(0x94D049BB133111EB)
+    return x ^ _lsr(x, 31)
+
+
+def counter_uniform(seed: int, counter: int, env: torch.Tensor, idx: torch.Tensor, channel: int) -> torch.Tensor:
+    """Uniform (0, 1) float64 per element from a counter-based hash of (seed, decision counter, global env id,
+    element index, channel): the draw of an env's element depends on nothing else, so a row samples the same
+    actions whichever rank / batch position holds it (the multi-rank PPO learner relies on this)."""
+    key = _mix64(env.long() * _i64(0xD1B54A32D192ED03) + _i64(counter & ((1 << 64) - 1)))
+    key = _mix64(key ^ _i64(seed & ((1 << 64) - 1)) ^ _mix64(idx.long() * 2 + channel))
+    return (_lsr(key, 11).double() + 0.5) * (1.0 / (1 << 53))
+
+
+def gumbel_pick(logp: torch.Tensor, seg: torch.Tensor, nseg: int, generator=None,
+                u: torch.Tensor | None = None) -> torch.Tensor:
     """One categorical draw per segment from log-probabilities (-inf = excluded): Gumbel-max; returns the flat
-    row index per segment (-1 for segments without a candidate)."""
-    u = torch.rand(logp.shape, dtype=torch.float64, device=logp.device, generator=generator)
+    row index per segment (-1 for segments without a candidate). `u`: the uniforms (default: torch.rand with
+    `generator`)."""
+    if u is None:
+        u = torch.rand(logp.shape, dtype=torch.float64, device=logp.device, generator=generator)
     g = logp.double() - torch.log(-torch.log(u.clamp_min(1e-300)))
     best = torch.full((nseg,), -torch.inf, dtype=torch.float64, device=logp.device)
     best = best.scatter_reduce(0, seg, g, reduce="amax", include_self=True)
@@ -435,17 +464,28 @@ class DecimaScheduler(nn.Module):
         return torch.cumsum(b.stage_mask.long(), 0) - 1 - _excl(b.num_stage_acts)[b.node_env]
 
     @torch.no_grad()
-    def schedule(self, b: DagBatch, generator=None) -> dict[str, torch.Tensor]:
+    def schedule(self, b: DagBatch, generator=None, stream: tuple | None = None) -> dict[str, torch.Tensor]:
         """One decision per env (envs with no schedulable stage get stage_idx -1, num_exec 1). Returns device
         tensors: stage_idx i32 [B] (index among the env's schedulable stages), num_exec i32 [B] (already
         1 + the sampled exec action, DecimaActWrapper.action), job_idx i64 [B] (DAG index within the env),
-        exec_idx i64 [B], lgprob f32 [B] (utils.sample: log of the softmax probability, stage + exec)."""
+        exec_idx i64 [B], lgprob f32 [B] (utils.sample: log of the softmax probability, stage + exec).
+        `stream` = (seed, counter, global env ids i64 [B]) draws the Gumbel noise from counter_uniform
+        instead of `generator` (rank-independent sampling)."""
         B = b.num_envs
         dev = b.x.device
         h = self.encoder(b, per_obs_no_mp=True)
         scores = self.stage_policy_network.scores_all(b, h)
         _, logp = masked_softmax_stats(scores, b.stage_mask, b.node_env, B, clamp=False)
-        pick = gumbel_pick(logp, b.node_env, B, generator)  # flat node row per env
+        u_stage = u_exec = None
+        if stream is not None:
+            seed, counter, env_ids = stream
+            env_ids = env_ids.to(dev).long()
+            local = torch.arange(b.x.shape[0], device=dev) - _excl(b.num_nodes)[b.node_env]
+            u_stage = counter_uniform(seed, counter, env_ids[b.node_env], local, 0)
+            N = self.num_executors
+            u_exec = counter_uniform(seed, counter, env_ids[:, None].expand(B, N).reshape(-1),
+                                     torch.arange(N, device=dev).repeat(B), 1)
+        pick = gumbel_pick(logp, b.node_env, B, generator, u=u_stage)  # flat node row per env
         live = pick >= 0
         row = pick.clamp(min=0)
         stage_idx = torch.where(live, self._sched_rows(b)[row] if row.numel() and b.x.shape[0] else pick, -1)
@@ -456,7 +496,7 @@ class DecimaScheduler(nn.Module):
         elogp = torch.where(valid, elogp, torch.full_like(elogp, -torch.inf))
         N = self.num_executors
         seg = torch.arange(B, device=dev)[:, None].expand(B, N).reshape(-1)
-        epick = gumbel_pick(elogp.reshape(-1), seg, B, generator)
+        epick = gumbel_pick(elogp.reshape(-1), seg, B, generator, u=u_exec)
         ok = live & (epick >= 0)
         exec_idx = torch.where(ok, epick - envs * N, torch.zeros_like(epick))
         lg_stage = torch.where(live, logp[row] if b.x.shape[0] else torch.zeros(B, device=dev),

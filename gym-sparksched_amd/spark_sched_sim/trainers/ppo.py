@@ -1,35 +1,40 @@
 """PPO on GPU rollouts (trainers/ppo.py:45-138 on top of trainers/trainer.py:28-190).
 
-One process per GPU. Each rank owns `num_sequences` job sequences x `num_rollouts` rollouts (all rollouts of a
-sequence on one GPU, so the Baseline interpolation stays local) as rows of one vector env, and a
-replica of the policy. Per iteration:
-  1. collect: RolloutCollector runs every row to the end of its episode (device-side reset with the
-     sequence's seed, Decima forward per decision, ssim_step);
-  2. returns (ReturnsCalculator) and baselines (Baseline) on device; advantages = returns - baselines;
-  3. PPO epochs over shuffled minibatches (num_batches per epoch): evaluate_actions with grads, CLIP loss with
-     the entropy bonus; gradients all-reduced (averaged) across ranks in one flat bucket over RCCL, then
-     clip_grad_norm + optimizer step on every replica (identical updates keep replicas equal); the
-     minibatch advantage normalisation and the approx-KL early stop use all-reduced statistics so every
-     rank takes the same decisions;
-  4. episode statistics (avg job duration, avg #jobs, completed / arrived jobs) all-gathered to every rank.
-Seeds follow trainer.py:258-262 / rollout_worker.py:118-120: row (sequence s, rollout r) of rank k uses
-seed + global_sequence + num_sequences_total * iteration.
+The reference runs `num_sequences x num_rollouts` rollout processes and ONE learner: the learner scatters the
+state dict, gathers every worker's RolloutBuffer, computes returns and baselines over all of them and runs the
+PPO epochs (trainer.py:85-162, ppo.py:51-103). Here, with one process per GPU:
+  1. the num_sequences x num_rollouts rows (row = sequence s, rollout r; s-major as trainer.py:268-270) are split
+     into contiguous blocks over the ranks; each rank's block is one vector env on its GPU, collected by
+     RolloutCollector (device-side reset with the row's seed, Decima forward per decision, ssim_step). Actions
+     are drawn from a counter-based stream keyed by the GLOBAL row, so a row's trajectory does not depend on
+     the world size;
+  2. each rank orders its samples row-major (row, decision) and the blocks are gathered over RCCL to the
+     learner (rank 0), which then holds exactly the batch a 1-rank run holds, in the same order;
+  3. the learner computes returns (ReturnsCalculator) and baselines (Baseline over all rows of a sequence),
+     advantages = returns - baselines, and runs the PPO epochs (shuffled minibatches, CLIP loss with the entropy
+     bonus, target-KL early stop, TrainableScheduler.update_parameters);
+  4. the learner broadcasts the updated parameters (the reference's state-dict scatter); episode statistics are
+     all-gathered (rollout_worker.py:122-129).
+Seeds follow trainer.py:258-270 / rollout_worker.py:118-120: row (s, r) uses seed + s + num_sequences *
+iteration. A multi-rank run therefore takes the same iteration as a 1-rank run of the same global config
+(tests/test_trainers.py checks the parameters bit for bit on 2 gloo ranks).
 """
 
 from __future__ import annotations
 
-import math
 from typing import Any
 
 import numpy as np
 import torch
 
-from .. import _abi
-from ..schedulers.decima import DecimaScheduler, select_envs
+from ..distributed import all_gather_var, split_rows
+from ..schedulers.decima import DagBatch, DecimaScheduler, cat_batches, select_envs
 from .returns import Baseline, ReturnsCalculator
 from .rollouts import AsyncRolloutCollector, RolloutCollector
 
 EPS = 1e-8  # ppo.py:13
+_BATCH_TENSORS = ["x", "edge_index", "edge_bits", "env_levels", "ptr", "node_dag", "node_env", "dag_env", "obs_ptr",
+                  "stage_mask", "exec_cap", "num_stage_acts", "num_nodes", "num_edges"]
 
 
 def _dist():
@@ -38,11 +43,27 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() else None
 
 
-def _allreduce_(t: torch.Tensor, op="sum") -> torch.Tensor:
-    d = _dist()
-    if d is not None and d.get_world_size() > 1:
-        d.all_reduce(t, op=d.ReduceOp.MAX if op == "max" else d.ReduceOp.SUM)
-    return t
+def gather_batches(b: DagBatch, world: int) -> DagBatch:
+    """Every rank's DagBatch concatenated in rank order (all_gather of each field, then cat_batches)."""
+    if world <= 1:
+        return b
+    parts = {}
+    for name in _BATCH_TENSORS:
+        t = getattr(b, name)
+        if name == "edge_index":
+            parts[name] = [p.t() for p in all_gather_var(t.t().contiguous(), world)]
+        elif name in ("ptr", "obs_ptr"):  # drop the leading 0 for the variable gather, restore per rank
+            parts[name] = [torch.cat([torch.zeros(1, dtype=p.dtype, device=p.device), p])
+                           for p in all_gather_var(t[1:].contiguous(), world)]
+        else:
+            parts[name] = all_gather_var(t, world)
+    scal = torch.tensor([b.max_levels, b.num_envs, b.max_nodes], dtype=torch.int64, device=b.x.device)
+    scals = all_gather_var(scal[None, :], world)
+    bs = []
+    for k in range(world):
+        ml, ne, mn = (int(v) for v in scals[k][0].tolist())
+        bs.append(DagBatch(**{n: parts[n][k] for n in _BATCH_TENSORS}, max_levels=ml, num_envs=ne, max_nodes=mn))
+    return cat_batches(bs)
 
 
 class PPO:
@@ -53,8 +74,8 @@ class PPO:
         self.world = d.get_world_size() if d else 1
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.seed = int(train_cfg["seed"])
-        torch.manual_seed(self.seed)  # identical initial replicas on every rank (trainer.py:33)
-        self.num_sequences = int(train_cfg["num_sequences"])  # per rank
+        torch.manual_seed(self.seed)  # identical initial policy on every rank (trainer.py:33)
+        self.num_sequences = int(train_cfg["num_sequences"])  # global, as in the reference config
         self.num_rollouts = int(train_cfg["num_rollouts"])
         self.num_iterations = int(train_cfg.get("num_iterations", 1))
         self.entropy_coeff = float(train_cfg.get("entropy_coeff", 0.0))
@@ -64,7 +85,7 @@ class PPO:
         self.num_batches = int(train_cfg.get("num_batches", 3))
         assert ("reward_buff_cap" in train_cfg) ^ ("beta_discount" in train_cfg), \
             "must provide exactly one of `reward_buff_cap` and `beta_discount` in config"
-        env_cfg = {k: v for k, v in env_cfg.items() if k != "dataset"}
+        env_cfg = dict(env_cfg)
         if "beta_discount" in train_cfg:
             env_cfg["beta"] = float(train_cfg["beta_discount"])
             self.return_calc = ReturnsCalculator(beta=float(train_cfg["beta_discount"]))
@@ -72,33 +93,37 @@ class PPO:
             self.return_calc = ReturnsCalculator(buff_cap=int(train_cfg["reward_buff_cap"]))
         self.env_cfg = env_cfg
         self.mean_time_limit = env_cfg.get("mean_time_limit")
-        self.baseline = Baseline(self.num_sequences, self.num_rollouts)
+        self.rows = self.num_sequences * self.num_rollouts
+        if self.rows < self.world:
+            raise ValueError(f"{self.rows} rollout rows cannot be split over {self.world} ranks")
+        self.row_lo, self.row_hi = split_rows(self.rows, self.world, self.rank)
+        self.baseline = Baseline(self.num_sequences, self.num_rollouts)  # learner side, over all rows
         kw = {k: v for k, v in agent_cfg.items() if k != "agent_cls"}
         self.scheduler = DecimaScheduler(env_cfg["num_executors"], opt_cls=train_cfg.get("opt_cls", "Adam"),
                                          opt_kwargs=train_cfg.get("opt_kwargs"),
                                          max_grad_norm=train_cfg.get("max_grad_norm"), **kw).to(self.device)
-        B = self.num_sequences * self.num_rollouts
+        B = self.row_hi - self.row_lo
         if dataset is None:
-            from ..data_samplers.synthetic_tpch import generate
+            from ..env import resolve_dataset
 
-            dataset = generate(0)
+            dataset = resolve_dataset(env_cfg)  # the config's data sampler (TPC-H, warns if it falls back)
+        sim_cfg = {k: v for k, v in env_cfg.items() if k not in ("mean_time_limit", "dataset")}
         if engine_factory is None:
             from ..engine import DeviceEngine
 
             def engine_factory(cfg, n, ds):
                 return DeviceEngine(cfg, n, ds, device=self.device)
-        self.engine = engine_factory({k: v for k, v in env_cfg.items() if k != "mean_time_limit"}, B, dataset)
+        self.engine = engine_factory(sim_cfg, B, dataset)
         self.rollout_duration = train_cfg.get("rollout_duration")  # trainer.py:63, async workers :277-279
+        rseed = self.seed * 7919
         if self.rollout_duration:
-            S_tot = self.num_sequences * self.world
-            base = [self.seed + self.rank * self.num_sequences + s for s in range(self.num_sequences)
-                    for _ in range(self.num_rollouts)]
-            self.collector = AsyncRolloutCollector(self.engine, self.scheduler, self.rollout_duration, base, S_tot,
-                                                   mean_time_limit=self.mean_time_limit,
-                                                   seed=self.seed * 7919 + self.rank)
+            base = [self.seed + r // self.num_rollouts for r in range(self.row_lo, self.row_hi)]
+            self.collector = AsyncRolloutCollector(self.engine, self.scheduler, self.rollout_duration, base,
+                                                   self.num_sequences, mean_time_limit=self.mean_time_limit,
+                                                   seed=rseed, row_offset=self.row_lo)
         else:
-            self.collector = RolloutCollector(self.engine, self.scheduler, seed=self.seed * 7919 + self.rank)
-        self.gen = torch.Generator(device=self.device).manual_seed(self.seed * 7919 + self.rank)
+            self.collector = RolloutCollector(self.engine, self.scheduler, seed=rseed, row_offset=self.row_lo)
+        self.gen = torch.Generator(device=self.device).manual_seed(rseed)  # learner's minibatch shuffling
         self.time_limit_rngs = None
         if self.mean_time_limit:
             # one StochasticTimeLimit per row, seeded like the reference wrapper (seed=42, reseeded by reset seed)
@@ -107,14 +132,10 @@ class PPO:
 
     # ------------------------------------------------------------------ rollouts
     def _seeds(self) -> list[int]:
-        """rollout_worker.py:118-120 with trainer.py:258-262's base seeds: sequence s gets
-        seed + s_global + S_total * reset_count, shared by its num_rollouts rows."""
-        S_tot = self.num_sequences * self.world
-        out = []
-        for s in range(self.num_sequences):
-            sg = self.rank * self.num_sequences + s
-            out += [self.seed + sg + S_tot * self.reset_count] * self.num_rollouts
-        return out
+        """rollout_worker.py:118-120 with trainer.py:258-270's base seeds: sequence s = row // num_rollouts gets
+        seed + s + num_sequences * reset_count, shared by its num_rollouts rows (this rank's rows only)."""
+        return [self.seed + r // self.num_rollouts + self.num_sequences * self.reset_count
+                for r in range(self.row_lo, self.row_hi)]
 
     def _time_limits(self, seeds):
         if not self.time_limit_rngs:
@@ -129,23 +150,76 @@ class PPO:
     def collect(self):
         self.scheduler.eval()
         if self.rollout_duration:
-            return self.collector.collect(generator=self.gen)
+            return self.collector.collect()
         seeds = self._seeds()
-        buf = self.collector.collect(seeds, self._time_limits(seeds), generator=self.gen)
+        buf = self.collector.collect(seeds, self._time_limits(seeds))
         self.reset_count += 1
         return buf
 
     # ------------------------------------------------------------------ learning
-    def train_on_rollouts(self, buf) -> dict[str, Any]:
+    def gather_rollouts(self, buf):
+        """This rank's buffer in row-major (row, decision) order, gathered over all ranks to one batch in global
+        row order: (times [R, T+1], rewards [R, T], lengths [R], obs DagBatch, actions) on every rank."""
         times, rewards, lengths, sample = buf.trajectories()
-        returns = self.return_calc(times, rewards, lengths)
-        base = self.baseline(times[:, :-1], returns, lengths)
-        valid = sample >= 0
-        n = len(buf)
-        advg = torch.zeros(n, dtype=torch.float64, device=returns.device)
-        advg[sample[valid]] = (returns - base)[valid]
         obs, acts = buf.samples()
-        return self._train(obs, acts, advg.float())
+        canon = sample[sample >= 0]  # row-major: row r's decisions in order, rows ascending
+        obs = select_envs(obs, canon)
+        acts = {k: v[canon] for k, v in acts.items()}
+        if self.world > 1:
+            T = torch.tensor([rewards.shape[1]], dtype=torch.int64, device=rewards.device)
+            Tm = int(max(int(t.item()) for t in all_gather_var(T, self.world)))
+            pad = Tm - rewards.shape[1]
+            if pad:
+                times = torch.cat([times, torch.zeros((times.shape[0], pad), dtype=times.dtype,
+                                                      device=times.device)], dim=1)
+                rewards = torch.cat([rewards, torch.zeros((rewards.shape[0], pad), dtype=rewards.dtype,
+                                                          device=rewards.device)], dim=1)
+            times = torch.cat(all_gather_var(times, self.world))
+            rewards = torch.cat(all_gather_var(rewards, self.world))
+            lengths = torch.cat(all_gather_var(lengths, self.world))
+            obs = gather_batches(obs, self.world)
+            acts = {k: torch.cat(all_gather_var(v, self.world)) for k, v in acts.items()}
+        return times, rewards, lengths, obs, acts
+
+    def train_on_rollouts(self, buf) -> dict[str, Any]:
+        times, rewards, lengths, obs, acts = self.gather_rollouts(buf)
+        info = None
+        if self.rank == 0:  # the learner (trainer.py:126-131, ppo.py:51-71)
+            returns = self.return_calc(times, rewards, lengths)
+            base = self.baseline(times[:, :-1], returns, lengths)
+            valid = torch.arange(rewards.shape[1], device=rewards.device)[None, :] < lengths[:, None]
+            advg = (returns - base)[valid]  # row-major = the gathered sample order
+            info = self._train(obs, acts, advg.float())
+        elif isinstance(self.return_calc.buff_cap, int) and self.return_calc.buff_cap:
+            self.return_calc(times, rewards, lengths)  # keep the differential-return window in step
+        self._broadcast_parameters()
+        return self._broadcast_info(info)
+
+    def _broadcast_parameters(self):
+        """The learner's parameters to every rank (trainer.py:110-111's state-dict scatter)."""
+        d = _dist()
+        if d is None or self.world == 1:
+            return
+        with torch.no_grad():
+            flat = torch.cat([p.detach().reshape(-1) for p in self.scheduler.parameters()])
+            d.broadcast(flat, src=0)
+            o = 0
+            for p in self.scheduler.parameters():
+                k = p.numel()
+                p.copy_(flat[o: o + k].view_as(p))
+                o += k
+
+    def _broadcast_info(self, info):
+        d = _dist()
+        if d is None or self.world == 1:
+            return info
+        t = torch.zeros(4, dtype=torch.float64, device=self.device)
+        if info is not None:
+            t[:] = torch.tensor([info["policy loss"], info["entropy"], info["approx kl div"], info["samples"]],
+                                dtype=torch.float64)
+        d.broadcast(t, src=0)
+        v = t.tolist()
+        return {"policy loss": v[0], "entropy": v[1], "approx kl div": v[2], "samples": int(v[3])}
 
     def _train(self, obs, acts, advg) -> dict[str, Any]:
         n = obs.num_envs
@@ -156,7 +230,7 @@ class PPO:
         for _ in range(self.num_epochs):
             if not cont:
                 break
-            perm = torch.randperm(n, device=advg.device, generator=self.gen)
+            perm = torch.randperm(n, device=advg.device, generator=self.gen)  # DataLoader(shuffle=True)
             for k in range(0, n, bs):
                 idx = perm[k: k + bs]
                 loss, info = self._loss(select_envs(obs, idx), {a: t[idx] for a, t in acts.items()}, advg[idx])
@@ -164,46 +238,30 @@ class PPO:
                 ent_losses.append(info["entropy_loss"])
                 kls.append(info["approx_kl_div"])
                 if self.target_kl is not None and info["approx_kl_div"] > 1.5 * self.target_kl:
-                    cont = False  # every rank sees the same all-reduced KL
+                    cont = False  # ppo.py:88-91
                     break
                 self._update(loss)
         return {"policy loss": abs(float(np.mean(pol_losses))), "entropy": abs(float(np.mean(ent_losses))),
                 "approx kl div": abs(float(np.mean(kls))), "samples": n}
 
     def _loss(self, obs, acts, advg):
+        """CLIP loss (ppo.py:105-138)."""
         ev = self.scheduler.evaluate_actions(obs, acts["stage_idx"], acts["job_idx"], acts["exec_idx"])
-        # minibatch advantage normalisation (ppo.py:118-119) over all ranks' minibatches
-        st = torch.stack([advg.sum().double(), (advg.double() ** 2).sum(), torch.tensor(float(advg.numel()),
-                          dtype=torch.float64, device=advg.device)])
-        _allreduce_(st)
-        m = st[0] / st[2]
-        var = (st[1] - st[2] * m * m) / torch.clamp(st[2] - 1, min=1)
-        a = (advg - m.float()) / (var.clamp(min=0).sqrt().float() + EPS)
+        a = (advg - advg.mean()) / (advg.std() + EPS)  # ppo.py:118-119
         log_ratio = ev["lgprobs"] - acts["lgprob"]
         ratio = log_ratio.exp()
         pl = -torch.min(a * ratio, a * torch.clamp(ratio, 1 - self.clip_range, 1 + self.clip_range)).mean()
         el = -ev["entropies"].mean()
         loss = pl + self.entropy_coeff * el
         with torch.no_grad():
-            red = torch.stack([pl.detach().double(), el.detach().double(), ((ratio - 1) - log_ratio).mean().double()])
-            _allreduce_(red)
-            red /= self.world
-        return loss, {"policy_loss": float(red[0]), "entropy_loss": float(red[1]), "approx_kl_div": float(red[2])}
+            kl = ((ratio - 1) - log_ratio).mean()
+        return loss, {"policy_loss": float(pl.detach()), "entropy_loss": float(el.detach()),
+                      "approx_kl_div": float(kl)}
 
     def _update(self, loss):
-        """TrainableScheduler.update_parameters (scheduler.py:34-53) with a data-parallel gradient average."""
+        """TrainableScheduler.update_parameters (scheduler.py:34-53)."""
         s = self.scheduler
         loss.backward()
-        params = [p for p in s.parameters() if p.grad is not None]
-        if self.world > 1 and params:
-            flat = torch.cat([p.grad.reshape(-1) for p in params])
-            _allreduce_(flat)
-            flat /= self.world
-            o = 0
-            for p in params:
-                k = p.grad.numel()
-                p.grad.copy_(flat[o: o + k].view_as(p.grad))
-                o += k
         if s.max_grad_norm:
             torch.nn.utils.clip_grad_norm_(s.parameters(), s.max_grad_norm, error_if_nonfinite=True)
         s.optim.step()
@@ -212,29 +270,13 @@ class PPO:
     # ------------------------------------------------------------------ statistics
     def episode_stats(self) -> torch.Tensor:
         """rollout_worker.py:122-129 per row: [avg job duration (s), avg #jobs, completed, arrived], gathered
-        from every rank (RCCL all_gather): [world * rows, 4]."""
-        eng = self.engine
-        if hasattr(eng, "job_times") and isinstance(eng.views["counts"], torch.Tensor):
-            ta, tc, st = eng.job_times()
-            wall = eng.views["wall_time"].double()
-        else:
-            a, c, s_ = eng.job_times_np()
-            ta, tc, st = (torch.from_numpy(x).to(self.device) for x in (a, c, s_))
-            wall = torch.from_numpy(np.asarray(eng.host_views()["wall_time"])).to(self.device).double()
-        arrived = st > 0
-        end = torch.where(st == 2, tc, wall[:, None].expand_as(tc))
-        dur = torch.where(arrived, torch.minimum(end, wall[:, None]) - ta, torch.zeros_like(ta))
-        n_done = (st == 2).sum(1)
-        # SparkSchedSimEnv.avg_job_duration (spark_sched_sim.py:243-245): mean completed-job duration, seconds
-        avg_jd = torch.where(st == 2, tc - ta, torch.zeros_like(ta)).sum(1) / n_done.clamp(min=1) * 1e-3
-        avg_jobs = dur.sum(1) / wall.clamp(min=1e-12)
-        mine = torch.stack([avg_jd, avg_jobs, n_done.double(), arrived.sum(1).double()], dim=1)
-        d = _dist()
-        if d is None or self.world == 1:
+        from every rank (RCCL all_gather) in global row order: [rows, 4]. avg job duration is the mean over
+        the last 200 completed jobs of the row's env across its episodes (spark_sched_sim.py:83,243-245,697;
+        the collector keeps the window, RolloutCollector.duration_window)."""
+        mine = self.collector.row_stats()
+        if self.world == 1:
             return mine
-        parts = [torch.empty_like(mine) for _ in range(self.world)]
-        d.all_gather(parts, mine.contiguous())
-        return torch.cat(parts)
+        return torch.cat(all_gather_var(mine, self.world))
 
     def train(self, num_iterations: int | None = None, log=print) -> list[dict]:
         hist = []
@@ -242,7 +284,8 @@ class PPO:
             buf = self.collect()
             stats = self.episode_stats()
             learn = self.train_on_rollouts(buf)
-            avg_jobs = float(stats[:, 1].mean())
+            # Trainer.train (trainer.py:135-137): the return calculator's moving average if it has one
+            avg_jobs = self.return_calc.avg_num_jobs or float(stats[:, 1].mean())
             rec = {"iteration": i, "avg_num_jobs": avg_jobs, "avg_job_duration": float(stats[:, 0].mean()),
                    "completed_jobs": float(stats[:, 2].mean()), **learn}
             hist.append(rec)

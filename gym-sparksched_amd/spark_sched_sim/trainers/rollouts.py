@@ -84,19 +84,32 @@ class RolloutCollector:
     """Drives a DeviceEngine (or the test-only HostEngine) with a DecimaScheduler until every env is done."""
 
     def __init__(self, engine, policy, num_tasks_scale: float = 200.0, work_scale: float = 1e5, fused: bool = True,
-                 seed: int = 0):
+                 seed: int = 0, row_offset: int = 0):
         self.engine = engine
         self.policy = policy
+        # global id of the engine's env 0: actions are sampled from a counter-based stream of (seed, decision
+        # counter, global row), so a row draws the same actions whichever rank holds it
+        self.row_offset = int(row_offset)
         self.scales = (num_tasks_scale, work_scale)
         from ..schedulers.decima import DECIMA_PARAMS
 
         # the fused kernel implements the decima_tpch.yaml architecture only
         self.fused = fused and sum(p.numel() for p in policy.parameters()) == DECIMA_PARAMS
         self.seed = seed
+        # decision counter of the sampling stream: (collect call << 32) + decision index within the call. A row
+        # takes its k-th decision of a call at loop step k on any rank, so the stream is rank-independent.
+        self.calls = 0
         self.counter = 0
         self.on_device = isinstance(engine.views["counts"], torch.Tensor)  # DeviceEngine vs test host build
         self._params = None  # packed policy weights, valid during one collect()
         self._pre = None  # (views, feats, live ids, batch sizes) fetched by _live for the next step
+        from ..metrics import RowStats
+
+        self.stats = RowStats(engine.num_envs)  # per-row collect_stats, duration windows across episodes
+
+    def row_stats(self) -> torch.Tensor:
+        """rollout_worker.py:122-129 per row, float64 [B, 4] on the policy's device (metrics.RowStats)."""
+        return torch.from_numpy(self.stats.stats(self.engine)).to(self.policy.device)
 
     def _views(self, features: bool = True):
         eng = self.engine
@@ -131,13 +144,18 @@ class RolloutCollector:
             self.counter += 1
             if self._params is None:  # weights are fixed for a whole collect(): pack them once
                 self._params = self.policy.packed_params(eng.device)
-            fo = self.policy.schedule_fused(eng, f, seed=self.seed, counter=self.counter, env_mask=alive,
+            # the kernel hashes (local env * C + counter); adding row_offset * C to the counter makes that the
+            # hash of the global row (C = 0x9E3779B97F4A7C15, csrc/decima_policy.h decima_policy_env)
+            ctr = (self.counter + self.row_offset * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+            fo = self.policy.schedule_fused(eng, f, seed=self.seed, counter=ctr, env_mask=alive,
                                             node_cap=batch.max_nodes, params=self._params)
             act = {"stage_idx": fo["stage_idx"], "num_exec": fo["num_exec"], "job_idx": fo["job_idx"].long(),
                    "exec_idx": fo["exec_idx"].long(), "lgprob": fo["lgprob"]}
         else:
             b_all = build_batch(v, f, env_mask=alive)
-            act = self.policy.schedule(b_all, generator=generator)
+            self.counter += 1
+            rows = self.row_offset + torch.arange(b_all.num_envs, device=b_all.x.device)
+            act = self.policy.schedule(b_all, stream=(self.seed, self.counter, rows))
             batch = b_all if all_alive else select_envs(b_all, envs)
         si = torch.where(alive, act["stage_idx"], torch.full_like(act["stage_idx"], -2))
         if self.on_device:
@@ -168,9 +186,12 @@ class RolloutCollector:
         """RolloutWorkerSync.collect_rollout (rollout_worker.py:135-157): reset every env with its seed,
         step until each env's episode ends."""
         self._params = None  # re-pack the (possibly updated) policy weights
+        self.calls += 1
+        self.counter = self.calls << 32
         eng = self.engine
         B = eng.num_envs
         limits = None if time_limits is None else torch.as_tensor(time_limits, dtype=torch.float64)
+        self.stats.flush(range(B), eng)  # the finished episodes' completions enter the duration windows
         eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds,
                           time_limits=None if limits is None else limits.cpu().numpy())
         v, _ = self._views(features=False)
@@ -217,6 +238,7 @@ class AsyncRolloutCollector(RolloutCollector):
         seeds = np.zeros(B, dtype=np.uint64)
         lim = np.full(B, np.inf)
         mode[env_ids] = _abi.SSIM_RESET_SEED
+        self.stats.flush(env_ids, self.engine)  # the finished episodes' completions enter the duration windows
         for e in env_ids:
             seeds[e] = int(self.base_seeds[e] + self.seed_step * self.reset_count[e])
             if self.limits is not None:
@@ -227,6 +249,8 @@ class AsyncRolloutCollector(RolloutCollector):
     @torch.no_grad()
     def collect(self, generator=None, max_steps: int = 10**9) -> GpuRolloutBuffer:
         self._params = None  # re-pack the (possibly updated) policy weights
+        self.calls += 1
+        self.counter = self.calls << 32
         B = self.engine.num_envs
         if self.next_wall is None:  # first call: reset every worker (rollout_worker.py:174-176)
             self._reset(np.arange(B))

@@ -33,6 +33,9 @@ class SparkSchedSimVecEnv:
         self.num_envs = num_envs
         self.device_reset = (num_envs >= DEVICE_RESET_MIN_ENVS) if device_reset is None else bool(device_reset)
         self._ever_reset = np.zeros(num_envs, dtype=bool)
+        from .metrics import RowStats
+
+        self.stats = RowStats(num_envs)
         self.num_executors = env_cfg["num_executors"]
         self.engine = DeviceEngine(env_cfg, num_envs, dataset, device=device, job_cap=job_cap, trace_cap=trace_cap)
         self.device = self.engine.device
@@ -58,6 +61,7 @@ class SparkSchedSimVecEnv:
         if self._limits is not None:
             options = [{"time_limit": self._limits.sample(i, None if seeds is None else seeds[k])}
                        for k, i in enumerate(ids)]
+        self.stats.flush(ids, self.engine)  # finished episodes' completions enter the duration windows
         if self.device_reset:
             self._reset_on_device(ids, seeds, options)
         else:
@@ -115,20 +119,12 @@ class SparkSchedSimVecEnv:
                 "decisions": c[:, _abi.OC_DECISIONS], "num_completed_jobs": c[:, _abi.OC_NUM_COMPLETED]}
 
     def episode_stats(self):
-        """Per-env stats as in trainers/rollout_worker.py:122-129 (avg job duration over this episode's
-        completed jobs, avg number of jobs in system, completed and arrived job counts), float64 [B, 4]."""
+        """Per-env stats as trainers/rollout_worker.py:122-129 collect_stats (metrics.RowStats): avg job duration
+        over the env's last 200 completed jobs across episodes (s), avg number of jobs in the system this episode,
+        completed and arrived job counts; float64 [B, 4] on the env's device."""
         import torch
 
-        ta, tc, st = self.engine.job_times()
-        wall = self.engine.views["wall_time"][:, None]
-        arrived = st > 0
-        end = torch.where(st == 2, tc, wall.expand_as(tc))
-        dur = torch.where(arrived, end - ta, torch.zeros_like(ta))
-        n_done = (st == 2).sum(1)
-        done_dur = torch.where(st == 2, dur, torch.zeros_like(dur)).sum(1)
-        avg_jd = done_dur / n_done.clamp(min=1) * 1e-3
-        avg_jobs = dur.sum(1) / wall[:, 0].clamp(min=1e-12)
-        return torch.stack([avg_jd, avg_jobs, n_done.double(), arrived.sum(1).double()], dim=1)
+        return torch.from_numpy(self.stats.stats(self.engine)).to(self.device)
 
     def close(self):
         self.engine.close()

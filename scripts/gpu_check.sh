@@ -19,6 +19,8 @@ for s in "$@"; do
   case "$s" in
     smoke)   step smoke 300 python __graft_entry__.py ;;
     pytest)  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    pytestk) step pytest_k 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PYTEST_K" ;;
+    bench_driver) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     bench)   step bench 400 python bench.py ;;
     bench_nocpu) step bench_nocpu 300 python bench.py --no-cpu-baseline ;;
     bench_step) step bench_step 300 python bench.py --no-cpu-baseline --mode step ;;

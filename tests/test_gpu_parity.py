@@ -102,3 +102,114 @@ def test_full_size_large_shard_replay(make, dataset, env_cfg):
     kernel compiled for 4 waves/SIMD): 40 fused decisions per env, every 512th env replayed on the oracle."""
     cfg = dict(env_cfg, num_executors=100, job_arrival_cap=200)
     cases.case_rollout_replay(make, dataset, cfg, _abi.SSIM_POLICY_RANDOM, B=4096, K=40, stride=512)
+
+
+@pytest.mark.parametrize("name", __import__("test_golden").NAMES)
+def test_golden_fixtures_device(gpu_device, dataset, name):
+    """The committed golden fixtures (tests/golden/*.json) replayed through the device engine step by step:
+    obs digests, wall times, rewards, the full event trace and job times."""
+    from spark_sched_sim.engine import DeviceEngine
+    from test_golden import load, replay_on_engine
+
+    fx = load(name)
+    eng = DeviceEngine(fx["cfg"], 1, dataset, device=gpu_device, trace_cap=fx["trace_len"] + 16)
+    replay_on_engine(eng, fx)
+
+
+def test_env_facade_device(gpu_device, dataset, env_cfg):
+    """The single-env facade on the device (test_env_facade.py runs the same checks on the host build):
+    a fair episode and a second one, observation space membership and the 200-job duration window."""
+    from oracle import restatement as R
+    from oracle.policies import FairPolicy
+    from spark_sched_sim.env import SparkSchedSimEnv
+    from test_env_facade import run_facade_vs_oracle
+
+    env = SparkSchedSimEnv(env_cfg, dataset, device=gpu_device)
+    ref = R.SparkSchedOracle(env_cfg, dataset)
+    for seed in (1234, 99, 5, 6, 7):
+        assert run_facade_vs_oracle(env, ref, FairPolicy(10), seed=seed) > 100
+        assert env.avg_job_duration == pytest.approx(ref.avg_job_duration, rel=1e-12)
+    obs, _ = env.reset(seed=3)
+    assert env.observation_space.contains(obs)
+
+
+@pytest.mark.parametrize("B", [1024])
+def test_vec_env_device_reset(gpu_device, dataset, env_cfg, B):
+    """SparkSchedSimVecEnv.reset through ONE ssim_reset_sampled launch (B >= 1024) gives exactly the host-sampled
+    reset (numpy Generator), for reset(seed) with StochasticTimeLimit limits and for reset(seed=None)."""
+    import numpy as np
+
+    from spark_sched_sim.vec_env import SparkSchedSimVecEnv
+
+    cfg = dict(env_cfg, job_arrival_cap=None)
+    kw = dict(device=gpu_device, job_cap=200, mean_time_limit=5.0e5)
+    dev = SparkSchedSimVecEnv(cfg, B, dataset, device_reset=True, **kw)
+    host = SparkSchedSimVecEnv(cfg, B, dataset, device_reset=False, **kw)
+    assert SparkSchedSimVecEnv(env_cfg, B, dataset, device=gpu_device).device_reset  # the default at this size
+    dev.reset(seed=100)
+    host.reset(seed=100)
+    assert np.array_equal(dev.engine.snapshot_obs(), host.engine.snapshot_obs())
+    for _ in range(20):
+        si, ne = host.policy(_abi.SSIM_POLICY_FAIR)
+        host.step(si, ne)
+        dev.step(si, ne)
+    dev.reset()
+    host.reset()
+    assert np.array_equal(dev.engine.snapshot_obs(), host.engine.snapshot_obs())
+    c = dev.engine.host_views()["counts"]
+    assert int(np.count_nonzero(c[:, _abi.OC_ERR])) == 0 and (c[:, _abi.OC_EPISODE] == 2).all()
+
+
+def test_full_size_decima_config2(gpu_device, dataset):
+    """BASELINE configs[2] at full size: 4096 envs, decima_tpch.yaml env section (N=50, J cap 200, StochasticTimeLimit
+    mean 2e7 ms), the fused Decima policy (LDS plan forced above 64 KB, the opt-in path) + ssim_step for K
+    decisions: no env errors, no policy overflow, and every 512th env's logged actions replayed on the oracle
+    reproduce its final observation, wall time and decision count bit-exactly."""
+    import numpy as np
+    import torch
+
+    import parity
+    from oracle.restatement import SparkSchedOracle
+    from spark_sched_sim.engine import DeviceEngine, obs_dict
+    from spark_sched_sim.schedulers.decima import DecimaScheduler
+    from spark_sched_sim.wrappers import StochasticTimeLimitSampler
+
+    cfg = dict(num_executors=50, job_arrival_cap=200, job_arrival_rate=4.0e-5, moving_delay=2000.0,
+               warmup_delay=1000.0)
+    B, K = 4096, 48
+    dev = torch.device(gpu_device)
+    eng = DeviceEngine(cfg, B, dataset, device=gpu_device)
+    seeds = [6000 + i for i in range(B)]
+    smp = StochasticTimeLimitSampler(2.0e7, B, seed=42)
+    limits = np.array([smp.sample(i, seeds[i]) for i in range(B)])
+    eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=limits)
+    torch.manual_seed(0)
+    pol = DecimaScheduler(50).to(dev)
+    packed = pol.packed_params(dev)
+    log = torch.zeros((K, B, 2), dtype=torch.int32, device=dev)
+    big_plan = 0
+    for k in range(K):
+        feats = eng.decima_features()
+        nodes = int(eng.views["counts"][:, _abi.OC_NUM_NODES].max().item())
+        cap = max(nodes, 400)  # 400 nodes x ~199 B + the per-DAG rows > 64 KB
+        fo = pol.schedule_fused(eng, feats, seed=11, counter=k, node_cap=cap, params=packed)
+        assert int(fo["overflow"].item()) == 0, f"step {k}"
+        big_plan += 1
+        log[k, :, 0] = fo["stage_idx"]
+        log[k, :, 1] = fo["num_exec"]
+        eng.step(fo["stage_idx"], fo["num_exec"])
+    assert big_plan == K
+    v = eng.host_views()
+    c = v["counts"]
+    assert int(np.count_nonzero(c[:, _abi.OC_ERR])) == 0
+    assert int(c[:, _abi.OC_NUM_NODES].max()) > 20
+    lg = log.cpu().numpy()
+    for i in range(0, B, 512):
+        o = SparkSchedOracle(cfg, dataset)
+        ob, _ = o.reset(seed=seeds[i], options={"time_limit": float(limits[i])})
+        n = int(c[i, _abi.OC_DECISIONS])
+        for k in range(n):
+            ob, _, term, _, _ = o.step({"stage_idx": int(lg[k, i, 0]), "num_exec": int(lg[k, i, 1])})
+        assert n == K or term, f"env{i}: {n} decisions"
+        assert float(v["wall_time"][i]) == float(o.wall_time)
+        parity.compare_obs(ob, obs_dict(v, i), f"env{i} final")

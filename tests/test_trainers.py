@@ -134,7 +134,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _ppo_rank(rank, world, port, q):
+def _ppo_rank(rank, world, port, q, train):
     for p in (HERE, REPO, os.path.join(REPO, "gym-sparksched_amd")):
         sys.path.insert(0, p)
     import torch.distributed as dist
@@ -142,38 +142,58 @@ def _ppo_rank(rank, world, port, q):
     from spark_sched_sim.data_samplers.synthetic_tpch import generate
     from spark_sched_sim.trainers import PPO
 
+    torch.set_num_threads(1)  # same intra-op threading as the 1-rank reference run (reduction order)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        ppo = PPO({"embed_dim": 16}, dict(SMALL_ENV, mean_time_limit=4e5), TRAIN, engine_factory=_host_engine,
+        ppo = PPO({"embed_dim": 16}, dict(SMALL_ENV, mean_time_limit=4e5), train, engine_factory=_host_engine,
                   dataset=generate(0), device="cpu")
         seeds = ppo._seeds()
-        ppo.train(1, log=None)
+        hist = ppo.train(2, log=None)
         flat = torch.cat([p.detach().reshape(-1) for p in ppo.scheduler.parameters()]).numpy()
-        q.put((rank, flat, seeds, ppo.episode_stats().numpy()))
+        q.put((rank, flat, seeds, ppo.episode_stats().numpy(), hist[-1]["samples"]))
     finally:
         dist.destroy_process_group()
 
 
-def test_ppo_two_rank_gloo_replicas_stay_identical():
+@pytest.mark.parametrize("train", [TRAIN, dict(TRAIN, num_sequences=3, num_rollouts=1)],
+                         ids=["2x2-rows", "3x1-rows-uneven"])
+def test_ppo_two_rank_gloo_equals_one_rank(dataset, train):
+    """the multi-rank iteration IS the reference's single-learner iteration. Rows are split
+    over 2 gloo ranks, trajectories gathered to rank 0, which learns and broadcasts; after 2 iterations every
+    rank's parameters equal a 1-rank run of the same global config bit for bit."""
     from hostsim.driver import build
+    from spark_sched_sim.trainers import PPO
 
     build()
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        one = PPO({"embed_dim": 16}, dict(SMALL_ENV, mean_time_limit=4e5), train, engine_factory=_host_engine,
+                  dataset=dataset, device="cpu")
+        seeds1 = one._seeds()
+        h1 = one.train(2, log=None)
+        stats1 = one.episode_stats().numpy()
+    finally:
+        torch.set_num_threads(threads)
+    ref = torch.cat([p.detach().reshape(-1) for p in one.scheduler.parameters()]).numpy()
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_ppo_rank, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ppo_rank, args=(r, world, port, q, train)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(world):
-        r, flat, seeds, st = q.get(timeout=600)
-        res[r] = (flat, seeds, st)
+        r, flat, seeds, st, n = q.get(timeout=600)
+        res[r] = (flat, seeds, st, n)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert np.array_equal(res[0][0], res[1][0])  # gradient all-reduce keeps the replicas bit-identical
-    assert res[0][1] != res[1][1] and set(res[0][1]).isdisjoint(res[1][1])  # disjoint job sequences per rank
-    assert np.array_equal(res[0][2], res[1][2]) and res[0][2].shape == (8, 4)  # gathered stats
+    assert res[0][1] + res[1][1] == seeds1  # rows split contiguously, seeds by global row
+    for r in range(world):
+        assert np.array_equal(res[r][0], ref), f"rank {r} parameters differ from the 1-rank learner"
+        assert res[r][3] == h1[-1]["samples"]
+        assert np.array_equal(res[r][2], stats1)  # gathered stats in global row order
 
 
 @pytest.mark.gpu
@@ -295,3 +315,56 @@ def test_cat_batches_equals_select_of_all(dataset):
         for name in got.__dataclass_fields__:
             a, b = getattr(want, name), getattr(got, name)
             assert (a.dtype == b.dtype and torch.equal(a, b)) if isinstance(a, torch.Tensor) else a == b, name
+
+
+@pytest.mark.gpu
+def test_ppo_decima_tpch_iteration_gpu(gpu_device, dataset):
+    """BASELINE configs[4] on the device: one PPO iteration of config/decima_tpch.yaml (4 sequences x 4 rollouts,
+    N=50, J cap 200, beta 5e-3, the Decima architecture through the fused policy kernel; mean time limit shortened
+    to 1e6 ms so the oracle replay stays short). Checks:
+      * returns and baselines of the gathered batch equal the numpy restatement of returns_calculator.py /
+        baselines.py (oracle/trainer_utils.py) within 1e-12 relative;
+      * every other row's logged actions replayed on the oracle (StochasticTimeLimit seeded as the trainer does)
+        reproduce its wall times bit for bit, its rewards within 1e-9 and its episode length exactly;
+      * the learner's update runs (finite losses) and changes the parameters."""
+    from oracle.restatement import SparkSchedOracle
+    import parity
+    from spark_sched_sim.trainers import DECIMA_TPCH, PPO
+
+    cfg = {k: dict(v) for k, v in DECIMA_TPCH.items()}
+    cfg["env"]["mean_time_limit"] = 1.0e6
+    ppo = PPO(cfg["agent"], cfg["env"], cfg["trainer"], dataset=dataset, device=gpu_device)
+    assert ppo.collector.fused
+    seeds = ppo._seeds()
+    buf = ppo.collect()
+    times, rewards, lengths, obs, acts = ppo.gather_rollouts(buf)
+    R = ppo.rows
+    assert R == 16 and int(lengths.min()) > 5
+    ret = ppo.return_calc(times, rewards, lengths)
+    base = ppo.baseline(times[:, :-1], ret, lengths)
+    n = lengths.cpu().numpy()
+    tl = [times[i, : n[i] + 1].cpu().numpy() for i in range(R)]
+    rl = [rewards[i, : n[i]].cpu().numpy() for i in range(R)]
+    ref_ret = TU.discounted_returns(tl, rl, 5.0e-3)
+    ref_base = TU.baseline_average([t[:-1] for t in tl], ref_ret, 4, 4)
+    for i in range(R):
+        assert np.allclose(ret[i, : n[i]].cpu().numpy(), ref_ret[i], rtol=1e-12, atol=1e-9), f"row {i} returns"
+        assert np.allclose(base[i, : n[i]].cpu().numpy(), ref_base[i], rtol=1e-12, atol=1e-6), f"row {i} baseline"
+    si, ei = acts["stage_idx"].cpu().numpy(), acts["exec_idx"].cpu().numpy()
+    off = np.concatenate([[0], np.cumsum(n)])
+    env_cfg = {k: v for k, v in ppo.env_cfg.items() if k not in ("mean_time_limit", "dataset")}
+    for i in range(0, R, 2):
+        limit = float(np.random.RandomState(seeds[i]).exponential(1.0e6))
+        o = SparkSchedOracle(env_cfg, dataset)
+        o.reset(seed=seeds[i], options={"time_limit": limit})
+        for k in range(n[i]):
+            j = off[i] + k
+            _, rew, term, _, info = o.step({"stage_idx": int(si[j]), "num_exec": 1 + int(ei[j])})
+            assert float(times[i, k + 1]) == info["wall_time"], f"row {i} step {k} wall"
+            assert parity.close_rel(float(rewards[i, k]), rew), f"row {i} step {k} reward"
+            assert (term or info["wall_time"] >= limit) == (k == n[i] - 1), f"row {i} step {k} episode end"
+    before = torch.cat([p.detach().reshape(-1) for p in ppo.scheduler.parameters()]).clone()
+    info = ppo.train_on_rollouts(buf)
+    after = torch.cat([p.detach().reshape(-1) for p in ppo.scheduler.parameters()])
+    assert np.isfinite(info["policy loss"]) and info["samples"] == int(n.sum())
+    assert not torch.equal(before, after)
