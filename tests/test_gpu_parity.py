@@ -142,7 +142,7 @@ def test_vec_env_device_reset(gpu_device, dataset, env_cfg, B):
     from spark_sched_sim.vec_env import SparkSchedSimVecEnv
 
     cfg = dict(env_cfg, job_arrival_cap=None)
-    kw = dict(device=gpu_device, job_cap=200, mean_time_limit=5.0e5)
+    kw = dict(device=gpu_device, job_cap=400, mean_time_limit=5.0e5)  # > 400 jobs needs a 20-mean limit
     dev = SparkSchedSimVecEnv(cfg, B, dataset, device_reset=True, **kw)
     host = SparkSchedSimVecEnv(cfg, B, dataset, device_reset=False, **kw)
     assert SparkSchedSimVecEnv(env_cfg, B, dataset, device=gpu_device).device_reset  # the default at this size
