@@ -14,7 +14,9 @@ Timeline of one run (all launches on one stream, inputs resident in HBM before a
   4. timed: exactly `--steps` steps (launches of `--chunk` steps, default one), bracketed by barrier +
      synchronize; HIP events on the launch stream time the kernels for the roofline.
 Modes: `rollout` (default: K steps = K x envs decisions of policy+step fused into one launch, claimed from a
-shared budget so envs with cheap decisions take more and the launch has no tail; `--lockstep` gives every env
+shared budget so envs with cheap decisions take more; once the budget is claimed, steps still simulating stop at
+their next event boundary and complete in the next launch (SSIM_ROLLOUT_PREEMPT), so a launch ends within ~one
+event instead of ~the longest step; decisions are counted when they complete; `--lockstep` gives every env
 exactly K) and `step` (two launches per step, the C-ABI call pattern of an external policy).
 
 Multi-GPU: `--gpus N` with no torchrun environment spawns N worker processes itself (one per GPU, before any
@@ -418,8 +420,8 @@ def main():
     def rollout_launch(c):
         if args.lockstep:
             eng.rollout(kind, 1234, c, flags=flags, time_limits=limits)
-        else:  # the same B x c decisions, claimed by whichever env is ready (no tail)
-            eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=flags, time_limits=limits)
+        else:  # the same B x c decisions, claimed by whichever env is ready; preemptible at event boundaries
+            eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=flags | _abi.SSIM_ROLLOUT_PREEMPT, time_limits=limits)
 
     def run(n, events=None, chunk=None):
         """n steps; `events` (list of HIP event pairs) brackets each kernel launch on the launch stream."""
@@ -536,7 +538,8 @@ def main():
                        else "device random",
                        "steps_per_launch": (args.chunk or K) if mode == "rollout" else 1,
                        "work_sharing": ("lockstep" if args.lockstep else "shared budget of envs x steps "
-                                        "decisions per launch") if mode == "rollout" else None,
+                                        "decisions per launch, preemptible at event boundaries")
+                       if mode == "rollout" else None,
                        "preroll": {"bound": preroll, "mean_decisions": float(pre_steps.mean())},
                        "autoreset": bool(mode != "step" and (flags or mode == "decima")),
                        "parallelism": f"env-sharded x{world}"},

@@ -58,7 +58,9 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
                  kPhSample, kPhPool, kPhScan, kPhLoadSave, kPhPoolBig, kPhIdleOrder, kPhDraw, kPhJobArr,
                  kPhExecArr, kPhTaskDone, kPhStageDone,
                  // event counters (not cycles)
-                 kCtPoolSmall, kCtPoolBig, kCtTask, kCtIdleOrder, kNumPhases };
+                 kCtPoolSmall, kCtPoolBig, kCtTask, kCtIdleOrder,
+                 // histogram of whole-decision cycles (policy + step + auto-reset): bucket b = [2^(b+10), 2^(b+11))
+                 kHist0, kNumPhases = kHist0 + 16 };
 #ifdef SSIM_PROFILE
 #define SSIM_COUNT(ph) prof[ph] += 1
 #else
@@ -74,6 +76,16 @@ enum : int32_t { kScanAll = 0, kScanOnly = 1, kScanExcept = 2 };
 struct StepIn {
   int32_t stage_idx, num_exec;
 };
+
+// Preemption policy of a step's simulation (Sim::simulate): `issue()` starts the (asynchronous) read of the stop
+// condition, `hit(v)` tests a value issued one event earlier, so the read's latency overlaps an event's work.
+// NoStop: steps always run to completion (every launch but the preemptible budget rollout).
+struct NoStop {
+  static constexpr bool kCan = false;
+  __device__ __forceinline__ uint64_t issue() const { return 0; }
+  __device__ __forceinline__ bool hit(uint64_t) const { return false; }
+};
+enum : int32_t { kSimIdle = 0, kSimDecision = 1, kSimPreempted = 2 };
 
 // Everything a launch needs besides the arenas. Lives at the start of the state arena (device memory),
 // so kernels take one pointer and read fields through the scalar cache.
@@ -133,6 +145,7 @@ struct Sim {
   int32_t eid;    // env index
   EnvHeader h;    // register copy of the header
   Pcg64 rng;
+  uint32_t iv_lane;  // Params::iv row `lane` (device: read with v_readlane instead of a scalar-cache load)
 #ifdef SSIM_PROFILE
   uint64_t prof[kNumPhases] = {0};
 #endif
@@ -145,7 +158,9 @@ struct Sim {
         ghot(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         cold(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes + O.hot_bytes),
-        scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index) {}
+        scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index) {
+    iv_lane = W::lane() < kIvRows ? *reinterpret_cast<const uint32_t*>(IV[W::lane()]) : 0u;
+  }
 
   // ---------------------------------------------------------------- hot-block residency
   __device__ __forceinline__ void copy16(uint8_t* dst, const uint8_t* src, int64_t bytes) {
@@ -828,9 +843,16 @@ struct Sim {
   // independent of the RNG) and the drawn duration; the executor key comes from Params::iv (scalar cache).
   __device__ __forceinline__ double task_duration(int n_local, int ts, int last, int lid, int keymask,
                                                   int maxlevel) {
+    return task_duration_dd(n_local, ts, last, lid, keymask, maxlevel, dur_gather(ts));
+  }
+  // task_duration with the descriptor gather already issued (the task-completion path issues it when the
+  // event is popped, so its latency overlaps the handler's LDS work)
+  __device__ __forceinline__ double task_duration_dd(int n_local, int ts, int last, int lid, int keymask,
+                                                     int maxlevel, const DurDesc& dd) {
     check(n_local > 0 && n_local < kIvRows);
-    const DurDesc dd = dur_gather(ts);
-    const uint32_t iv = W::uni(*reinterpret_cast<const uint32_t*>(IV[n_local < kIvRows ? n_local : 0]));
+    const int row = n_local < kIvRows ? n_local : 0;
+    const uint32_t iv = (W::kWidth == 64 && row < 64) ? (uint32_t)W::bcast_i((int)iv_lane, row)
+                                                      : W::uni(*reinterpret_cast<const uint32_t*>(IV[row]));
     const int lo = (int)(iv & 0xFF), hi = (int)((iv >> 8) & 0xFF);
     int level = (int)((iv >> 16) & 0xFF);  // key = lo
     if (lo != hi) {  // _sample_executor_key (tpch.py:216-235): one random() draw
@@ -932,6 +954,9 @@ struct Sim {
   // _execute_next_task (:584-615) on register copies of the stage and executor records (ld_rec), which the
   // caller writes back: the task-completion path then costs one LDS access per record, not one per field.
   __device__ __forceinline__ void run_next_task_rec(int g, StageRec& s, ExecRec& x) {
+    run_next_task_rec(g, s, x, dur_gather(s.ts));
+  }
+  __device__ __forceinline__ void run_next_task_rec(int g, StageRec& s, ExecRec& x, const DurDesc& dd) {
     const int j = s.job;
     check(s.rem > 0);
     check(x.job == j);
@@ -944,7 +969,7 @@ struct Sim {
     SSIM_COUNT(kCtTask);
     const int lid = g - jr.base;
     SSIM_MARK("sample_begin");
-    const double dur = task_duration(jr.local, s.ts, x.task, lid, s.fw_keymask, s.fw_maxlevel);
+    const double dur = task_duration_dd(jr.local, s.ts, x.task, lid, s.fw_keymask, s.fw_maxlevel, dd);
     SSIM_MARK("sample_end");
     SSIM_TOC(t_smp, kPhSample);
     x.task = (int16_t)lid;
@@ -1138,16 +1163,16 @@ struct Sim {
     trace(h.wall, kTrJobDone, -1, j, -1, -1);
   }
 
-  __device__ __forceinline__ void on_task_done(int e, int g) {  // :452-483
+  // `s` = the stage record (read when the event was popped), `dd` = its duration descriptors, in flight
+  __device__ __forceinline__ void on_task_done(int e, int g, StageRec s, const DurDesc& dd) {  // :452-483
     SSIM_MARK("task_done_begin");
-    StageRec s = ld_rec(stage(g));
     ExecRec x = ld_rec(exr(e));
     const int j = s.job;
     check(!(s.rem == 0 && s.exe == 0));
     s.exe = (int16_t)(s.exe - 1);
     x.busy = 0;
     if (s.rem > 0) {  // the common case: the executor takes the stage's next task
-      run_next_task_rec(g, s, x);
+      run_next_task_rec(g, s, x, dd);
       stage(g) = s;
       exr(e) = x;
       return;
@@ -1214,11 +1239,18 @@ struct Sim {
     return true;
   }
 
-  // Returns true when it stopped at a decision point (committable executors and a schedulable stage).
-  __device__ __forceinline__ bool simulate() {  // _resume_simulation :320-343
-    h.step_events = 0;
+  // kSimDecision when it stopped at a decision point (committable executors and a schedulable stage), kSimIdle
+  // when the queue ran dry (or the env froze), kSimPreempted when `stop` fired between two events (the state is
+  // then exactly the reference's between those events; a later call continues the loop).
+  template <class Stop>
+  __device__ __forceinline__ int simulate(const Stop& stop) {  // _resume_simulation :320-343
+    uint64_t tk = stop.issue();
     for (;;) {
-      if (frozen()) return false;
+      if (frozen()) return kSimIdle;
+      if (Stop::kCan) {
+        if (stop.hit(tk)) return kSimPreempted;
+        tk = stop.issue();  // read for the next event's check, in flight while this event is handled
+      }
       double t;
       int kind, e, g, seq;
       SSIM_TIC(t_pop);
@@ -1226,7 +1258,7 @@ struct Sim {
       const bool have = pop_event(&t, &kind, &e, &g, &seq);
       SSIM_MARK("pop_end");
       SSIM_TOC(t_pop, kPhPop);
-      if (!have) return false;
+      if (!have) return kSimIdle;
       SSIM_TIC(t_h);
       h.wall = t;
       h.events++;
@@ -1246,7 +1278,10 @@ struct Sim {
           on_executor_arrival(e, g);
           SSIM_TOC(t_x, kPhExecArr);
         } else {
-          on_task_done(e, g);
+          const StageRec sr = ld_rec(stage(g));
+          // the next task's duration descriptors (if the stage has tasks left): issued now, used after the
+          // executor / job record reads
+          on_task_done(e, g, sr, sr.rem > 0 ? dur_gather(sr.ts) : DurDesc{0, 0});
           SSIM_TOC(t_x, kPhTaskDone);
         }
       }
@@ -1262,7 +1297,7 @@ struct Sim {
         h.source = kPoolNone;
       }
       SSIM_TOC(t_s, kPhPostScan);
-      if (found) return true;
+      if (found) return kSimDecision;
     }
   }
 
@@ -1457,27 +1492,71 @@ struct Sim {
     step_loaded(a);
   }
   __device__ __forceinline__ bool idle() const { return h.terminated || frozen() || h.num_jobs == 0; }
-  // step() with the header already in registers (the fused rollout loads it once for policy + step)
-  __device__ __forceinline__ void step_loaded(StepIn a) {
-    if (h.terminated || frozen() || h.num_jobs == 0) return;
+  __device__ __forceinline__ EnvAcc& acc() const { return *H<EnvAcc>(O.acc); }
+  __device__ __forceinline__ bool pending() const { return W::uni(acc().pending) != 0; }
+  __device__ __forceinline__ void count_decision() {  // a step completed (its observation is written)
+    UF<int64_t> d{&acc().decisions};
+    d = (int64_t)d + 1;
+  }
+  // The end of a step from its simulation on: returns false if `stop` preempted it (pending, see EnvAcc).
+  template <class Stop>
+  __device__ __forceinline__ bool finish_step(double t0, const Stop& stop) {
+    const int r = simulate(stop);
+    if (Stop::kCan && r == kSimPreempted) {
+      W::sync();
+      if (W::lane() == 0) {
+        acc().pend_t0 = t0;
+        acc().pending = 1;
+      }
+      store_header();
+      write_err_only(SSIM_ERR_PENDING);
+      return false;
+    }
+    const double reward = -jobtime(t0, h.decisions);
+    h.terminated = (h.n_completed == h.num_jobs) ? 1 : 0;
+    // step's `assert committable and schedulable_stages` (:212-215): simulate() stopped at a decision
+    // point (state untouched since) unless the queue ran dry
+    if (!h.terminated) check(r == kSimDecision);
+    SSIM_TIC(t_o);
+    observe(reward);
+    SSIM_TOC(t_o, kPhObserve);
+    count_decision();
+    store_header();
+    return true;
+  }
+  // Completes a step preempted by an earlier launch (header loaded); true if none was pending or it completed.
+  template <class Stop>
+  __device__ __forceinline__ bool resume(const Stop& stop) {
+    if (!pending()) return true;
+    const double t0 = W::uni(acc().pend_t0);
+    W::sync();
+    if (W::lane() == 0) acc().pending = 0;
+    W::sync();
+    return finish_step(t0, stop);
+  }
+  // step() with the header already in registers (the fused rollout loads it once for policy + step). Returns
+  // false when `stop` preempted the step's simulation (the step stays pending until resume()).
+  template <class Stop = NoStop>
+  __device__ __forceinline__ bool step_loaded(StepIn a, const Stop& stop = Stop()) {
+    if (h.terminated || frozen() || h.num_jobs == 0) return true;
     SSIM_TIC(t_act);
     const int idx = a.stage_idx, nx = a.num_exec;
     // Discrete(n, start=-1) holds -1 .. n-2; Discrete(N, start=1) holds 1 .. N
     if (idx < -1 || idx > h.stage_idx_n - 2 || nx < 1 || nx > NE) {
       write_err_only(SSIM_ERR_SPACE);
-      return;
+      return true;
     }
     if (idx == -1) {
       commit_leftovers();
     } else {
       if (idx >= h.n_sched) {
         write_err_only(SSIM_ERR_KEY);
-        return;
+        return true;
       }
       const int g = ld(H<int16_t>(O.sched_list) + idx);
       if (nx > committable()) {
         write_err_only(SSIM_ERR_TOO_MANY);
-        return;
+        return true;
       }
       const int d = demand(g);
       const int n = nx < d ? nx : d;  // _adjust_num_executors
@@ -1493,10 +1572,6 @@ struct Sim {
       W::sync();
     }
     h.decisions++;
-    {
-      UF<int64_t> d{&H<EnvAcc>(O.acc)->decisions};
-      d = (int64_t)d + 1;
-    }
     h.step_events = 0;
     SSIM_TOC(t_act, kPhAction);
     SSIM_TIC(t_rc);
@@ -1506,8 +1581,9 @@ struct Sim {
       SSIM_TIC(t_o);
       observe(0.0);
       SSIM_TOC(t_o, kPhObserve);
+      count_decision();
       store_header();
-      return;
+      return true;
     }
     SSIM_TIC(t_f);
     commit_leftovers();
@@ -1523,17 +1599,7 @@ struct Sim {
       h.n_selected = 0;
       W::sync();
     }
-    const double t0 = h.wall;
-    const bool at_decision = simulate();
-    const double reward = -jobtime(t0, h.decisions);
-    h.terminated = (h.n_completed == h.num_jobs) ? 1 : 0;
-    // step's `assert committable and schedulable_stages` (:212-215): simulate() stopped at a decision
-    // point (state untouched since) unless the queue ran dry
-    if (!h.terminated) check(at_decision);
-    SSIM_TIC(t_o);
-    observe(reward);
-    SSIM_TOC(t_o, kPhObserve);
-    store_header();
+    return finish_step(h.wall, stop);
   }
 
   // ---------------------------------------------------------------- device-side reset sampling
@@ -1603,6 +1669,10 @@ struct Sim {
     if (W::uni(prev->num_jobs) > 0) {  // the previous episode ends here (accumulators persist, EnvAcc)
       UF<int64_t> eps{&H<EnvAcc>(O.acc)->episodes};
       eps = (int64_t)eps + 1;
+    }
+    {  // a step preempted in the previous episode is abandoned with it
+      UF<int64_t> pend{&H<EnvAcc>(O.acc)->pending};
+      pend = (int64_t)0;
     }
     h = EnvHeader();
     h.episode = prev_episode + 1;

@@ -49,10 +49,14 @@ struct EnvHeader {
 };
 static_assert(sizeof(EnvHeader) % 16 == 0, "header must keep 16-B alignment");
 
-// Running sums over observations (SURVEY.md §8d algorithmic-byte accounting), decisions and finished
-// episodes, kept across resets. Updated in place once per decision, never held in registers.
+// Running sums over observations (SURVEY.md §8d algorithmic-byte accounting), completed decisions and finished
+// episodes, kept across resets. Updated in place once per decision, never held in registers. `pending` /
+// `pend_t0`: a step preempted between two events of its simulation (ssim_rollout_budget with
+// SSIM_ROLLOUT_PREEMPT) and the wall time its reward interval starts at; the next launch completes it.
 struct EnvAcc {
-  int64_t nodes, edges, jobs, events, decisions, episodes, pad[2];
+  int64_t nodes, edges, jobs, events, decisions, episodes;
+  double pend_t0;
+  int64_t pending;
 };
 static_assert(sizeof(EnvAcc) % 16 == 0, "accumulator record");
 

@@ -64,6 +64,19 @@ __global__ __launch_bounds__(64) void k_reset_sampled(const Params* __restrict__
 #ifndef SSIM_HBM_STEP_WAVES
 #define SSIM_HBM_STEP_WAVES 4
 #endif
+// The preemptible budget rollout's stop condition: the shared decision counter has reached the budget. The load is
+// issued one event ahead of its test (Sim::simulate), so its latency hides behind that event's handling.
+struct TicketStop {
+  static constexpr bool kCan = true;
+  const unsigned long long* p;
+  int64_t budget;
+  bool on;
+  __device__ __forceinline__ uint64_t issue() const {
+    return on ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  }
+  __device__ __forceinline__ bool hit(uint64_t v) const { return on && (int64_t)WaveHip::uni(v) >= budget; }
+};
+
 template <bool kRes, int kN, int kJ, int kS>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_STEP_WAVES))) void k_step(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                              const int32_t* __restrict__ stage_idx,
@@ -75,7 +88,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
   a.stage_idx = stage_idx[eid];
   a.num_exec = num_exec[eid];
   s.load_hot();
-  s.step(a);
+  s.load_header();
+  if (s.pending()) {  // a preempted step completes first; this call's action (chosen on a stale obs) is dropped
+    s.resume(NoStop());
+    s.write_err_only(SSIM_ERR_PENDING);
+  } else {
+    s.step_loaded(a);
+  }
   s.save_hot();
 }
 
@@ -110,10 +129,23 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
   s.load_hot();
   // Shared budget (budget > 0): decisions are claimed from one device counter in chunks sized to what is
   // left (guided self-scheduling: 8 early, 1 at the end), so the launch ends within ~one decision of the
-  // budget running out instead of waiting for the env with the most expensive K decisions.
+  // budget running out instead of waiting for the env with the most expensive K decisions. With
+  // SSIM_ROLLOUT_PREEMPT it ends within ~one EVENT: a step still simulating when the budget runs out stops at
+  // its next event boundary and stays pending for the next launch.
   unsigned long long* tickets =
       budget > 0 ? reinterpret_cast<unsigned long long*>(state + kTicketOffset) : nullptr;
+  const TicketStop stop{tickets, budget, tickets != nullptr && (flags & SSIM_ROLLOUT_PREEMPT) != 0};
   int64_t granted = 0, last = 0;
+  s.load_header();
+  if (s.pending()) {  // a step preempted by the previous launch completes first (whatever this launch's mode)
+    if (!s.resume(stop)) {
+      s.save_hot();
+      return;
+    }
+    if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit))
+      s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
+                      reset + (int64_t)eid * P->L.reset_stride);
+  }
   for (int k = 0; k < num_steps; ++k) {
 #ifdef SSIM_PROFILE
     const uint64_t t0 = WaveHip::clock();
@@ -141,11 +173,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
       action_log[((int64_t)k * B + eid) * 2 + 1] = a.num_exec;
     }
     WaveHip::sync();
-    s.step_loaded(a);
+    if (!s.step_loaded(a, stop)) break;  // preempted mid-simulation: pending until the next launch
     // episode over (terminated, or truncated by the time limit): reset(seed=None) in place
     if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit))
       s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
                       reset + (int64_t)eid * P->L.reset_stride);
+#ifdef SSIM_PROFILE
+    {
+      const uint64_t dc = WaveHip::clock() - t0;
+      int b = 63 - __builtin_clzll(dc | 1ull) - 10;
+      b = b < 0 ? 0 : b > 15 ? 15 : b;
+      s.prof[kHist0 + b] += 1;
+    }
+#endif
   }
   s.save_hot();
 #ifdef SSIM_PROFILE
@@ -341,7 +381,10 @@ static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t n
   if (h == nullptr || num_steps < 0 || budget < 0) return set_err(SSIM_E_ARG, "ssim_rollout: bad argument");
   if (kind != SSIM_POLICY_FAIR && kind != SSIM_POLICY_FIFO && kind != SSIM_POLICY_RANDOM)
     return set_err(SSIM_E_ARG, "ssim_rollout: unknown policy %d", kind);
-  if ((flags & ~SSIM_ROLLOUT_AUTORESET) != 0) return set_err(SSIM_E_ARG, "ssim_rollout_ex: unknown flags 0x%x", flags);
+  if ((flags & ~(SSIM_ROLLOUT_AUTORESET | SSIM_ROLLOUT_PREEMPT)) != 0)
+    return set_err(SSIM_E_ARG, "ssim_rollout_ex: unknown flags 0x%x", flags);
+  if ((flags & SSIM_ROLLOUT_PREEMPT) && budget <= 0)
+    return set_err(SSIM_E_ARG, "ssim_rollout: SSIM_ROLLOUT_PREEMPT needs a decision budget (ssim_rollout_budget)");
   if ((flags & SSIM_ROLLOUT_AUTORESET) && !(h->params.C.job_arrival_gap > 0.0))
     return set_err(SSIM_E_ARG, "ssim_rollout_ex: auto-reset needs job_arrival_gap in the config");
   const ssim_layout& L = h->params.L;

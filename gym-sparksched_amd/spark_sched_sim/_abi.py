@@ -8,9 +8,11 @@ SSIM_RESET_SKIP, SSIM_RESET_CONTINUE, SSIM_RESET_SEED = 0, 1, 2
 NUM_ACC = 8  # int64 accumulators per env (ob_acc): S_act, E_act, J_act, events, decisions, episodes, 0, 0
 ACC_NODES, ACC_EDGES, ACC_JOBS, ACC_EVENTS, ACC_DECISIONS, ACC_EPISODES = range(6)
 SSIM_ROLLOUT_AUTORESET = 0x1
+SSIM_ROLLOUT_PREEMPT = 0x2
 SSIM_ERR_SPACE = 0x1
 SSIM_ERR_KEY = 0x2
 SSIM_ERR_TOO_MANY = 0x4
+SSIM_ERR_PENDING = 0x8
 SSIM_ERR_INVARIANT = 0x10
 SSIM_ERR_CAPACITY = 0x20
 SSIM_ERR_SAMPLER = 0x40

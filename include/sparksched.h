@@ -30,6 +30,9 @@ extern "C" {
 #define SSIM_ERR_SPACE 0x1u       /* ValueError: action not in action space (spark_sched_sim.py:276-277) */
 #define SSIM_ERR_KEY 0x2u         /* KeyError: stage_idx >= #schedulable stages (spark_sched_sim.py:284) */
 #define SSIM_ERR_TOO_MANY 0x4u    /* ValueError: num_exec > committable executors (:294-295) */
+#define SSIM_ERR_PENDING 0x8u     /* the env's last step was preempted mid-simulation (SSIM_ROLLOUT_PREEMPT); the obs
+                                     arena still holds the previous observation; any ssim_rollout_* call or
+                                     ssim_step completes it (ssim_step then ignores its action for that env) */
 #define SSIM_ERR_INVARIANT 0x10u  /* an `assert` of the reference fired; env frozen */
 #define SSIM_ERR_CAPACITY 0x20u   /* a device capacity (commitments, trace) overflowed; env frozen */
 #define SSIM_ERR_SAMPLER 0x40u    /* task_duration found no durations (reference raises); env frozen */
@@ -184,6 +187,11 @@ int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
  * episode's limit is time_limits[env] (device float64 [num_envs], NULL = +inf). Each env's obs counts
  * carry its episode number (SSIM_OC_EPISODE). */
 #define SSIM_ROLLOUT_AUTORESET 0x1
+/* ssim_rollout_budget only: once the budget is spent, an env in the middle of a step stops at the next event
+ * boundary instead of finishing the step (the launch ends within ~one event rather than ~the longest step);
+ * the step stays pending (SSIM_ERR_PENDING) and the next launch on the handle completes it first. Decisions
+ * are counted when they complete (ob_acc), so back-to-back launches count every decision exactly once. */
+#define SSIM_ROLLOUT_PREEMPT 0x2
 int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
                     const double* time_limits, int32_t* action_log, void* stream);
 

@@ -30,6 +30,10 @@ for s in "$@"; do
     bench_large) step bench_large 400 python bench.py --workload large --steps 100 --warmup 20 ;;
     prof)    step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     phase)   step phase 600 python scripts/phase_profile.py ;;
+    sweep)   step sweep 900 bash scripts/steps_sweep.sh ;;
+    ab)      step ab 900 bash scripts/ab_tpch.sh ;;
+    ab20)    step ab20 900 env AB_TAG=s20 AB_ARGS="--steps 20 --warmup 5" bash scripts/ab_tpch.sh ;;
+    pmc)     step pmc 900 bash scripts/pmc_profile.sh ;;
     prof_step) step prof_step 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_step" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -17,7 +17,8 @@ sys.path.insert(0, os.path.join(REPO, "gym-sparksched_amd"))
 PHASES = ["policy", "action", "round_check", "fulfill", "pop", "handle", "post_scan", "observe",
           "(sample)", "(pool ops)", "(scans)", "(hot load/save)", "(big-table staging)", "(idle_order)",
           "(duration draw)", "(job arrival)", "(executor arrival)", "(task done)", "(stage completion)",
-          "#small-table ops", "#big-table ops", "#task launches", "#idle_order"]
+          "#small-table ops", "#big-table ops", "#task launches", "#idle_order"] + [
+          f"#decisions {1 << (b + 10)}-{1 << (b + 11)} cycles" for b in range(16)]
 TOP = 8  # the first TOP phases are disjoint; the rest are inclusive sub-timers
 
 
@@ -83,7 +84,10 @@ def main():
     print(f"decisions {dec}, events {e1 - e0} ({(e1 - e0) / dec:.2f}/decision)")
     top = tot[:TOP].sum()
     for name, v in zip(PHASES, tot):
-        print(f"  {name:16s} {v / dec:10.1f} cycles/decision  {100 * v / top:5.1f}%")
+        if name.startswith("#decisions"):
+            print(f"  {name:32s} {v / dec * 100:8.3f}% of decisions")
+        else:
+            print(f"  {name:16s} {v / dec:10.1f} cycles/decision  {100 * v / top:5.1f}%")
     res["phases_ticks_per_decision"] = {n: float(v / dec) for n, v in zip(PHASES, tot)}
     res["events_per_decision"] = (e1 - e0) / dec
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)

@@ -111,6 +111,59 @@ def case_rollout_replay(make, dataset, env_cfg, kind, B=64, K=400, stride=4, bud
             assert tc[i][jid] == job.t_completed or (np.isinf(tc[i][jid]) and np.isinf(job.t_completed))
 
 
+def case_rollout_preempt(make, dataset, env_cfg, B=64, launches=8, per_launch=25, autoreset=True):
+    """ssim_rollout_budget with SSIM_ROLLOUT_PREEMPT: once a launch's budget is claimed, steps still simulating
+    stop at their next event boundary and stay pending (SSIM_ERR_PENDING); the next launch completes them first.
+    Preemption must not change anything the env computes: each env's actions, logged launch by launch and
+    concatenated, replayed on the oracle give its final observation, wall time, decision count and event trace
+    bit for bit, after a closing launch (0 new steps) has completed the pending steps. Completed decisions
+    (ob_acc) across the launches add up to the decisions applied."""
+    SENT = -99
+    eng = make(env_cfg, B, dataset, 8000)
+    seeds = [6100 + i for i in range(B)]
+    eng.reset(seeds=seeds)
+    flags = _abi.SSIM_ROLLOUT_PREEMPT | (_abi.SSIM_ROLLOUT_AUTORESET if autoreset else 0)
+    K = 8 * per_launch
+    actions = [[] for _ in range(B)]
+    pending_seen = 0
+    for _ in range(launches):
+        log = eng.alloc_action_log(K)
+        log.fill_(SENT)
+        eng.rollout_budget(_abi.SSIM_POLICY_RANDOM, 17, K, B * per_launch, log, flags=flags)
+        lg = np.asarray(eng.to_numpy(log))
+        for i in range(B):
+            rows = lg[:, i, 0] != SENT
+            actions[i] += [(int(a), int(b)) for a, b in lg[rows, i]]
+        c = eng.host_views()["counts"]
+        pending_seen += int(np.count_nonzero(c[:, _abi.OC_ERR] & _abi.SSIM_ERR_PENDING))
+    assert pending_seen > B, pending_seen  # preemption actually happened, launch after launch
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 17, 0, flags=_abi.SSIM_ROLLOUT_AUTORESET if autoreset else 0)
+    v = eng.host_views()
+    assert int(np.count_nonzero(v["counts"][:, _abi.OC_ERR])) == 0  # nothing pending, no errors
+    applied = sum(len(a) for a in actions)
+    assert int(v["acc"][:, _abi.ACC_DECISIONS].sum()) == applied
+    episodes = 0
+    for i in range(0, B, 4):
+        o = SparkSchedOracle(env_cfg, dataset)
+        o.trace = []
+        ob, _ = o.reset(seed=seeds[i])
+        ep = 1
+        for a in actions[i]:
+            ob, rew, term, _, info = o.step({"stage_idx": a[0], "num_exec": a[1]})
+            if term and autoreset:
+                o.trace = []
+                ob, _ = o.reset(seed=None)
+                ep += 1
+        c = v["counts"][i]
+        assert int(c[_abi.OC_EPISODE]) == ep
+        assert float(v["wall_time"][i]) == float(o.wall_time), f"env{i}"
+        parity.compare_obs(ob, obs_dict(v, i), f"env{i} final")
+        got = decode_trace(np.asarray(v["trace"][i]), int(c[_abi.OC_TRACE_LEN]))
+        ref = [tuple(float(x) if j == 0 else int(x) for j, x in enumerate(r)) for r in o.trace]
+        assert got == ref[: len(got)] and len(ref) == int(c[_abi.OC_TRACE_LEN]), f"env{i} trace"
+        episodes += ep
+
+
 def case_invalid_actions(make, dataset, env_cfg, B=8):
     """ValueError/KeyError cases of _take_action (spark_sched_sim.py:276-295) -> per-env error bits, state
     untouched; a following valid action proceeds exactly like the oracle."""

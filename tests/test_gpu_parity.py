@@ -48,6 +48,11 @@ def test_rollout_budget_replay(make, dataset, env_cfg, kind):
     cases.case_rollout_replay(make, dataset, env_cfg, kind, B=64, K=400, stride=4, budget=150)
 
 
+@pytest.mark.parametrize("autoreset", [True, False])
+def test_rollout_preempt_replay(make, dataset, env_cfg, autoreset):
+    cases.case_rollout_preempt(make, dataset, env_cfg, autoreset=autoreset)
+
+
 def test_rollout_replay_full_episodes(make, dataset, env_cfg):
     cases.case_rollout_replay(make, dataset, env_cfg, _abi.SSIM_POLICY_RANDOM, B=256, K=2500, stride=32)
 
