@@ -65,6 +65,13 @@ WORKLOADS = {
                        "valid actions (BASELINE configs[3] per-GPU shard)"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# CPU-only reference config (BASELINE configs[0]): examples.py --sched fair, one env in one process
+CPU_ONLY = {"examples": dict(cfg=ENV_CFG, mean_time_limit=None, policy="fair",
+                             desc="examples.py --sched fair: one env, 50 jobs / 10 executors (BASELINE configs[0])")}
+
+
+def _workload(name: str) -> dict:
+    return WORKLOADS[name] if name in WORKLOADS else CPU_ONLY[name]
 
 
 # ------------------------------------------------------------------------------------------------ launcher
@@ -144,7 +151,7 @@ def _cpu_worker(args):
         torch.set_num_threads(1)  # rollout_worker.py:93
     except ImportError:
         torch = None
-    wl = WORKLOADS[workload]
+    wl = _workload(workload)
     cfg = wl["cfg"]
     env = SparkSchedOracle(cfg, generate(0))
     if wl["mean_time_limit"]:
@@ -207,7 +214,7 @@ def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0)
     wall = max(r[1] for r in res)
     host = os.cpu_count() or procs
     value = dec / wall
-    wl = WORKLOADS[workload]
+    wl = _workload(workload)
     return {"value": value, "unit": "decisions/s", "cores": procs, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus": host, "usable_cpus": usable_cpus(),
             "per_core": value / procs, "projected_host": value / procs * host,
@@ -328,6 +335,8 @@ def main():
     ap.add_argument("--lockstep", action="store_true",
                     help="rollout mode: every env takes exactly `chunk` decisions per launch (ssim_rollout_ex) "
                          "instead of sharing a budget of envs x chunk decisions (ssim_rollout_budget)")
+    ap.add_argument("--no-preempt", action="store_true",
+                    help="rollout mode: budget launches finish every started step (no SSIM_ROLLOUT_PREEMPT)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="rollout mode: leave finished envs idle instead of resetting them on the device")
     ap.add_argument("--engine", choices=["hip", "host"], default="hip",
@@ -421,7 +430,8 @@ def main():
         if args.lockstep:
             eng.rollout(kind, 1234, c, flags=flags, time_limits=limits)
         else:  # the same B x c decisions, claimed by whichever env is ready; preemptible at event boundaries
-            eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=flags | _abi.SSIM_ROLLOUT_PREEMPT, time_limits=limits)
+            pre = 0 if args.no_preempt else _abi.SSIM_ROLLOUT_PREEMPT
+            eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=flags | pre, time_limits=limits)
 
     def run(n, events=None, chunk=None):
         """n steps; `events` (list of HIP event pairs) brackets each kernel launch on the launch stream."""
@@ -538,7 +548,8 @@ def main():
                        else "device random",
                        "steps_per_launch": (args.chunk or K) if mode == "rollout" else 1,
                        "work_sharing": ("lockstep" if args.lockstep else "shared budget of envs x steps "
-                                        "decisions per launch, preemptible at event boundaries")
+                                        "decisions per launch" + ("" if args.no_preempt else
+                                                                  ", preemptible at event boundaries"))
                        if mode == "rollout" else None,
                        "preroll": {"bound": preroll, "mean_decisions": float(pre_steps.mean())},
                        "autoreset": bool(mode != "step" and (flags or mode == "decima")),

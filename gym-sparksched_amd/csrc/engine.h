@@ -60,7 +60,9 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
                  // event counters (not cycles)
                  kCtPoolSmall, kCtPoolBig, kCtTask, kCtIdleOrder,
                  // histogram of whole-decision cycles (policy + step + auto-reset): bucket b = [2^(b+10), 2^(b+11))
-                 kHist0, kNumPhases = kHist0 + 16 };
+                 kHist0,
+                 // s_memrealtime stamps (100 MHz chip clock): wave entry, hot block loaded, loop exit, hot block saved
+                 kTEntry = kHist0 + 16, kTLoaded, kTLoopEnd, kTSaved, kNumPhases };
 #ifdef SSIM_PROFILE
 #define SSIM_COUNT(ph) prof[ph] += 1
 #else
@@ -101,8 +103,13 @@ struct Params {
   uint8_t iv[kIvRows][4];
 };
 constexpr int64_t kParamsReserve = 4096;
-// The last 64 B of the params block hold the shared-budget rollout's decision counter (ssim_rollout_budget).
-constexpr int64_t kTicketOffset = kParamsReserve - 64;
+// The last 1 KB of the params block holds the shared-budget rollouts' decision counters (ssim_rollout_budget):
+// two slots used alternately, each with kTicketShards counters on separate 64-B lines (one per XCD group of envs,
+// env e -> shard e % kTicketShards, the round-robin workgroup-to-XCD dispatch order).
+constexpr int kTicketShards = 8;
+constexpr int64_t kTicketOffset = kParamsReserve - 1024;
+constexpr int64_t kTicketStride = 64;
+constexpr int64_t kTicketSlotBytes = kTicketShards * kTicketStride;
 static_assert(sizeof(Params) <= kTicketOffset, "params block");
 
 __host__ __device__ inline int exec_level_index(double key) {  // EXEC_LEVELS index, 0xFF if not a level
@@ -1242,14 +1249,22 @@ struct Sim {
   // kSimDecision when it stopped at a decision point (committable executors and a schedulable stage), kSimIdle
   // when the queue ran dry (or the env froze), kSimPreempted when `stop` fired between two events (the state is
   // then exactly the reference's between those events; a later call continues the loop).
+  // The stop condition is a read of one shared word (TicketStop): polled every kStopEvery-th event, issued one
+  // event before it is tested so its latency hides behind that event. Most steps take fewer events and finish
+  // unpolled; the long ones (hundreds of task events) are the launch tail preemption removes.
+  static constexpr int kStopEvery = 8;
   template <class Stop>
   __device__ __forceinline__ int simulate(const Stop& stop) {  // _resume_simulation :320-343
-    uint64_t tk = stop.issue();
+    uint64_t tk = 0;
+    int n = 0;
     for (;;) {
       if (frozen()) return kSimIdle;
       if (Stop::kCan) {
-        if (stop.hit(tk)) return kSimPreempted;
-        tk = stop.issue();  // read for the next event's check, in flight while this event is handled
+        const int ph = n++ & (kStopEvery - 1);
+        if (ph == kStopEvery - 1)
+          tk = stop.issue();
+        else if (ph == 0 && n > 1 && stop.hit(tk))
+          return kSimPreempted;
       }
       double t;
       int kind, e, g, seq;
@@ -1517,46 +1532,59 @@ struct Sim {
     // step's `assert committable and schedulable_stages` (:212-215): simulate() stopped at a decision
     // point (state untouched since) unless the queue ran dry
     if (!h.terminated) check(r == kSimDecision);
+    count_decision();  // before observe(), which publishes the accumulators to the obs arena
     SSIM_TIC(t_o);
     observe(reward);
     SSIM_TOC(t_o, kPhObserve);
-    count_decision();
     store_header();
     return true;
+  }
+  // The pending step's reward-interval start; clears the pending mark (the caller then runs finish_step).
+  __device__ __forceinline__ double take_pending() {
+    const double t0 = W::uni(acc().pend_t0);
+    W::sync();
+    if (W::lane() == 0) acc().pending = 0;
+    W::sync();
+    return t0;
   }
   // Completes a step preempted by an earlier launch (header loaded); true if none was pending or it completed.
   template <class Stop>
   __device__ __forceinline__ bool resume(const Stop& stop) {
     if (!pending()) return true;
-    const double t0 = W::uni(acc().pend_t0);
-    W::sync();
-    if (W::lane() == 0) acc().pending = 0;
-    W::sync();
-    return finish_step(t0, stop);
+    return finish_step(take_pending(), stop);
   }
-  // step() with the header already in registers (the fused rollout loads it once for policy + step). Returns
-  // false when `stop` preempted the step's simulation (the step stays pending until resume()).
+  // step() with the header already in registers. Returns false when `stop` preempted the step's simulation (the
+  // step stays pending until resume()).
   template <class Stop = NoStop>
   __device__ __forceinline__ bool step_loaded(StepIn a, const Stop& stop = Stop()) {
-    if (h.terminated || frozen() || h.num_jobs == 0) return true;
+    double t0;
+    if (!step_begin(a, &t0)) return true;
+    return finish_step(t0, stop);
+  }
+  // The first part of a step: the action (:275-315) and, if the round continues, the observation. Returns true
+  // when the step goes on to simulate (finish_step from *t0), false when it is complete (or rejected / idle).
+  // The fused rollout calls step_begin and finish_step from one loop, so finish_step (the event loop, the
+  // observation) is inlined once whether a launch starts a step or completes a preempted one.
+  __device__ __forceinline__ bool step_begin(StepIn a, double* t0) {
+    if (h.terminated || frozen() || h.num_jobs == 0) return false;
     SSIM_TIC(t_act);
     const int idx = a.stage_idx, nx = a.num_exec;
     // Discrete(n, start=-1) holds -1 .. n-2; Discrete(N, start=1) holds 1 .. N
     if (idx < -1 || idx > h.stage_idx_n - 2 || nx < 1 || nx > NE) {
       write_err_only(SSIM_ERR_SPACE);
-      return true;
+      return false;
     }
     if (idx == -1) {
       commit_leftovers();
     } else {
       if (idx >= h.n_sched) {
         write_err_only(SSIM_ERR_KEY);
-        return true;
+        return false;
       }
       const int g = ld(H<int16_t>(O.sched_list) + idx);
       if (nx > committable()) {
         write_err_only(SSIM_ERR_TOO_MANY);
-        return true;
+        return false;
       }
       const int d = demand(g);
       const int n = nx < d ? nx : d;  // _adjust_num_executors
@@ -1578,12 +1606,12 @@ struct Sim {
     const bool round_continues = committable() > 0 && any_schedulable();
     SSIM_TOC(t_rc, kPhRoundCheck);
     if (round_continues) {
+      count_decision();
       SSIM_TIC(t_o);
       observe(0.0);
       SSIM_TOC(t_o, kPhObserve);
-      count_decision();
       store_header();
-      return true;
+      return false;
     }
     SSIM_TIC(t_f);
     commit_leftovers();
@@ -1599,7 +1627,8 @@ struct Sim {
       h.n_selected = 0;
       W::sync();
     }
-    return finish_step(h.wall, stop);
+    *t0 = h.wall;
+    return true;
   }
 
   // ---------------------------------------------------------------- device-side reset sampling

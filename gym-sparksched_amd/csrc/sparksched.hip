@@ -64,6 +64,8 @@ __global__ __launch_bounds__(64) void k_reset_sampled(const Params* __restrict__
 #ifndef SSIM_HBM_STEP_WAVES
 #define SSIM_HBM_STEP_WAVES 4
 #endif
+constexpr int32_t kFlagTicketSlot = 0x100;  // internal k_rollout flag: use the second budget counter
+
 // The preemptible budget rollout's stop condition: the shared decision counter has reached the budget. The load is
 // issued one event ahead of its test (Sim::simulate), so its latency hides behind that event's handling.
 struct TicketStop {
@@ -118,6 +120,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
                                                 const int32_t* __restrict__ env_steps) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
+  if (budget > 0 && eid == 0 && WaveHip::lane() < kTicketShards)  // the next budget launch's counters (`tickets`)
+    *reinterpret_cast<unsigned long long*>(state + kTicketOffset + ((flags & kFlagTicketSlot) ? 0 : kTicketSlotBytes) +
+                                           kTicketStride * WaveHip::lane()) = 0ull;
   if (env_steps != nullptr) {  // per-env decision counts (ssim_rollout_steps), capped by num_steps
     const int n = env_steps[eid];
     num_steps = n < num_steps ? n : num_steps;
@@ -125,55 +130,78 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
   }
   const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   if (env_idle(P, state, eid) && action_log == nullptr && !autoreset) return;
+#ifdef SSIM_PROFILE
+  const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
   s.load_hot();
+#ifdef SSIM_PROFILE
+  s.prof[kTEntry] = rt_entry;
+  s.prof[kTLoaded] = __builtin_amdgcn_s_memrealtime();
+#endif
   // Shared budget (budget > 0): decisions are claimed from one device counter in chunks sized to what is
   // left (guided self-scheduling: 8 early, 1 at the end), so the launch ends within ~one decision of the
   // budget running out instead of waiting for the env with the most expensive K decisions. With
   // SSIM_ROLLOUT_PREEMPT it ends within ~one EVENT: a step still simulating when the budget runs out stops at
   // its next event boundary and stays pending for the next launch.
+  // Two counter slots used alternately (kFlagTicketSlot): this launch's start at 0 because the previous budget
+  // launch zeroed them, and this launch zeroes the other slot for the next (launches on a stream are ordered), so
+  // no memset launch precedes a budget launch. The budget is split over kTicketShards counters (env e claims from
+  // shard e % kTicketShards, its XCD under round-robin dispatch), so claims and the preemption polls spread over
+  // eight cache lines instead of queueing on one atomic word; each shard spends its share exactly.
+  const int slot = (flags & kFlagTicketSlot) ? 1 : 0;
+  const int shard = eid % kTicketShards;
+  const int nshard = B < kTicketShards ? B : kTicketShards;
+  const int shard_envs = B / nshard + (shard < B % nshard ? 1 : 0);
+  const bool budgeted = budget > 0;
+  if (budgeted) budget = budget / nshard + (shard < budget % nshard ? 1 : 0);  // this shard's share (may be 0)
   unsigned long long* tickets =
-      budget > 0 ? reinterpret_cast<unsigned long long*>(state + kTicketOffset) : nullptr;
+      budgeted ? reinterpret_cast<unsigned long long*>(state + kTicketOffset + kTicketSlotBytes * slot +
+                                                       kTicketStride * shard)
+               : nullptr;
+
   const TicketStop stop{tickets, budget, tickets != nullptr && (flags & SSIM_ROLLOUT_PREEMPT) != 0};
   int64_t granted = 0, last = 0;
-  s.load_header();
-  if (s.pending()) {  // a step preempted by the previous launch completes first (whatever this launch's mode)
-    if (!s.resume(stop)) {
-      s.save_hot();
-      return;
-    }
-    if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit))
-      s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
-                      reset + (int64_t)eid * P->L.reset_stride);
-  }
-  for (int k = 0; k < num_steps; ++k) {
+  // One loop both starts steps and completes a step a previous launch preempted (pending), so the simulation /
+  // observation code (finish_step) is inlined once.
+  for (int k = 0;;) {
 #ifdef SSIM_PROFILE
     const uint64_t t0 = WaveHip::clock();
 #endif
     s.load_header();
-    if (tickets != nullptr) {
-      if (!autoreset && (s.h.terminated || s.frozen())) break;
-      if (granted == 0) {
-        int64_t c = (budget - last) / (4 * (int64_t)B);
-        c = c < 1 ? 1 : c > 8 ? 8 : c;
-        unsigned long long t = 0;
-        if (WaveHip::lane() == 0) t = atomicAdd(tickets, (unsigned long long)c);
-        last = (int64_t)WaveHip::uni((uint64_t)t);
-        if (last >= budget) break;
-        granted = budget - last < c ? budget - last : c;
+    double st0 = 0.0;
+    bool simulate;
+    if (s.pending()) {  // completes first, whatever this launch's mode; not one of its num_steps
+      st0 = s.take_pending();
+      simulate = true;
+    } else {
+      if (k >= num_steps) break;
+      if (tickets != nullptr) {
+        if (!autoreset && (s.h.terminated || s.frozen())) break;
+        if (granted == 0) {
+          int64_t c = (budget - last) / (4 * (int64_t)shard_envs);
+          c = c < 1 ? 1 : c > 8 ? 8 : c;
+          unsigned long long t = 0;
+          if (WaveHip::lane() == 0) t = atomicAdd(tickets, (unsigned long long)c);
+          last = (int64_t)WaveHip::uni((uint64_t)t);
+          if (last >= budget) break;
+          granted = budget - last < c ? budget - last : c;
+        }
+        --granted;
       }
-      --granted;
-    }
-    const StepIn a = sim_policy(s, kind, seed);
+      const StepIn a = sim_policy(s, kind, seed);
 #ifdef SSIM_PROFILE
-    s.prof[kPhPolicy] += WaveHip::clock() - t0;
+      s.prof[kPhPolicy] += WaveHip::clock() - t0;
 #endif
-    if (action_log != nullptr && WaveHip::lane() == 0) {
-      action_log[((int64_t)k * B + eid) * 2 + 0] = a.stage_idx;
-      action_log[((int64_t)k * B + eid) * 2 + 1] = a.num_exec;
+      if (action_log != nullptr && WaveHip::lane() == 0) {
+        action_log[((int64_t)k * B + eid) * 2 + 0] = a.stage_idx;
+        action_log[((int64_t)k * B + eid) * 2 + 1] = a.num_exec;
+      }
+      ++k;
+      WaveHip::sync();
+      simulate = s.step_begin(a, &st0);
     }
-    WaveHip::sync();
-    if (!s.step_loaded(a, stop)) break;  // preempted mid-simulation: pending until the next launch
+    if (simulate && !s.finish_step(st0, stop)) break;  // preempted mid-simulation: pending until the next launch
     // episode over (terminated, or truncated by the time limit): reset(seed=None) in place
     if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit))
       s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
@@ -187,8 +215,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
     }
 #endif
   }
+#ifdef SSIM_PROFILE
+  s.prof[kTLoopEnd] = __builtin_amdgcn_s_memrealtime();
+#endif
   s.save_hot();
 #ifdef SSIM_PROFILE
+  s.prof[kTSaved] = __builtin_amdgcn_s_memrealtime();
   if (prof_out != nullptr && WaveHip::lane() == 0)
     for (int p = 0; p < kNumPhases; ++p) prof_out[(int64_t)eid * kNumPhases + p] = s.prof[p];
 #else
@@ -241,23 +273,22 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
   }
 }
 
-// Kernel variant for a layout: LDS-resident instantiations, fully specialised on (executors, jobs, stage cap)
-// for the benchmark shape (BASELINE configs[1]: 10 executors, 50 jobs, 50 x 18 stages of the TPC-H-format
-// dataset), else the generic ones.
+// Kernel variant for a layout: LDS-resident instantiations specialised on the benchmark shape (BASELINE configs[1]:
+// 10 executors, 50 jobs): fully (stage cap too) when the packed dataset's cap is the synthetic set's 50 x 18, else
+// on (executors, jobs) with the stage cap read at run time (any other TPC-H-format dataset, e.g. the real traces
+// loaded from data/tpch); other shapes use the generic instantiations.
 using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
 using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int, const double*, uint8_t*,
                           int32_t*, uint64_t*, int64_t, const int32_t*);
-static bool bench_shape(const Params& p) {
-  return p.L.num_executors == 10 && p.L.job_cap == 50 && p.L.stage_cap == 900;
-}
+static bool bench_shape(const Params& p) { return p.L.num_executors == 10 && p.L.job_cap == 50; }
 static StepFn pick_step(const Params& p) {
   if (!p.O.lds_resident) return k_step<false, 0, 0, 0>;
-  if (bench_shape(p)) return k_step<true, 10, 50, 900>;
+  if (bench_shape(p)) return p.L.stage_cap == 900 ? k_step<true, 10, 50, 900> : k_step<true, 10, 50, 0>;
   return k_step<true, 0, 0, 0>;
 }
 static RolloutFn pick_rollout(const Params& p) {
   if (!p.O.lds_resident) return k_rollout<false, 0, 0, 0>;
-  if (bench_shape(p)) return k_rollout<true, 10, 50, 900>;
+  if (bench_shape(p)) return p.L.stage_cap == 900 ? k_rollout<true, 10, 50, 900> : k_rollout<true, 10, 50, 0>;
   return k_rollout<true, 0, 0, 0>;
 }
 
@@ -267,6 +298,7 @@ struct ssim_handle {
   uint8_t* state;
   uint8_t* obs;
   uint8_t* reset;
+  int ticket_slot;  // budget-launch decision counter in use next (k_rollout kFlagTicketSlot)
 };
 
 static thread_local char g_err[512] = "";
@@ -389,8 +421,8 @@ static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t n
     return set_err(SSIM_E_ARG, "ssim_rollout_ex: auto-reset needs job_arrival_gap in the config");
   const ssim_layout& L = h->params.L;
   if (budget > 0) {
-    if (hip_check(hipMemsetAsync(h->state + kTicketOffset, 0, 8, (hipStream_t)stream), "ticket reset") != SSIM_OK)
-      return SSIM_E_HIP;
+    if (h->ticket_slot) flags |= kFlagTicketSlot;
+    h->ticket_slot ^= 1;
   }
   hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, flags, time_limits, h->reset, action_log,
@@ -442,6 +474,18 @@ extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed
                      dparams(h), h->state, h->obs, kind, seed, num_steps, 0, (const double*)nullptr, h->reset,
                      (int32_t*)nullptr, prof_out, (int64_t)0, (const int32_t*)nullptr);
   return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
+}
+// Diagnostic build only: the budget rollout (as bench.py) with per-wave phase sums and realtime stamps.
+extern "C" int ssim_rollout_budget_profiled(ssim_handle* h, int32_t kind, uint64_t seed, int32_t max_steps,
+                                            int64_t total_decisions, int32_t flags, uint64_t* prof_out,
+                                            void* stream) {
+  const ssim_layout& L = h->params.L;
+  if (h->ticket_slot) flags |= kFlagTicketSlot;
+  h->ticket_slot ^= 1;
+  hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+                     dparams(h), h->state, h->obs, kind, seed, max_steps, flags, (const double*)nullptr, h->reset,
+                     (int32_t*)nullptr, prof_out, total_decisions, (const int32_t*)nullptr);
+  return hip_check(hipGetLastError(), "k_rollout(budget, profiled) launch");
 }
 #endif
 

@@ -32,6 +32,10 @@ for s in "$@"; do
     phase)   step phase 600 python scripts/phase_profile.py ;;
     sweep)   step sweep 900 bash scripts/steps_sweep.sh ;;
     ab)      step ab 900 bash scripts/ab_tpch.sh ;;
+    cpubase) step cpubase 900 python scripts/cpu_baselines.py ;;
+    abargs)  step abargs 900 bash scripts/ab_args.sh ;;
+    launch)  step launch 600 python scripts/launch_profile.py ;;
+    ab20np)  step ab20np 900 env AB_TAG=s20np AB_ARGS="--steps 20 --warmup 5 --no-preempt" bash scripts/ab_tpch.sh ;;
     ab20)    step ab20 900 env AB_TAG=s20 AB_ARGS="--steps 20 --warmup 5" bash scripts/ab_tpch.sh ;;
     pmc)     step pmc 900 bash scripts/pmc_profile.sh ;;
     prof_step) step prof_step 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_step" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step --steps 100 ;;

@@ -218,3 +218,13 @@ def test_full_size_decima_config2(gpu_device, dataset):
         assert n == K or term, f"env{i}: {n} decisions"
         assert float(v["wall_time"][i]) == float(o.wall_time)
         parity.compare_obs(ob, obs_dict(v, i), f"env{i} final")
+
+
+def test_rollout_replay_other_stage_cap(make, env_cfg):
+    """A TPC-H-format dataset whose largest query has 17 stages (stage cap 850, not the default set's 900) runs the
+    (executors, jobs)-specialised kernels with the stage cap read at run time; replayed on the oracle."""
+    from spark_sched_sim.data_samplers.synthetic_tpch import generate
+
+    ds = generate(1)
+    assert max(a.shape[0] for a, _ in ds.values()) == 17
+    cases.case_rollout_replay(make, ds, env_cfg, _abi.SSIM_POLICY_RANDOM, B=64, K=400, stride=8)
