@@ -410,11 +410,12 @@ def main():
     pre_steps = np.zeros(B, dtype=np.int32)
     if preroll > 0 and mode != "step":
         pre_steps = np.random.default_rng([args.seed, rank, 7]).integers(0, preroll, B).astype(np.int32)
-        eng.rollout_steps(kind, 4321, pre_steps, int(pre_steps.max()) + 1, flags=_abi.SSIM_ROLLOUT_AUTORESET,
-                          time_limits=limits)
+        eng.rollout_steps(kind, 4321, pre_steps, int(pre_steps.max()) + 1,
+                          flags=_abi.SSIM_ROLLOUT_AUTORESET | _abi.SSIM_ROLLOUT_WARMUP, time_limits=limits)
     elif preroll > 0:  # step mode: the same spread through the fused launch, then per-step launches
         pre_steps = np.random.default_rng([args.seed, rank, 7]).integers(0, preroll, B).astype(np.int32)
-        eng.rollout_steps(kind, 4321, pre_steps, int(pre_steps.max()) + 1, flags=0, time_limits=limits)
+        eng.rollout_steps(kind, 4321, pre_steps, int(pre_steps.max()) + 1, flags=_abi.SSIM_ROLLOUT_WARMUP,
+                          time_limits=limits)
 
     if mode == "decima":
         from spark_sched_sim.schedulers.decima import DecimaScheduler, build_batch
@@ -426,12 +427,13 @@ def main():
         packed = pol.packed_params(dev)  # fixed weights during rollouts: packed once, like RolloutCollector
         overflow_total = torch.zeros((), dtype=torch.int64, device=dev)
 
-    def rollout_launch(c):
+    def rollout_launch(c, timed):
+        f = flags | (0 if timed or host else _abi.SSIM_ROLLOUT_WARMUP)  # warm-up launches: k_rollout_warmup symbol
         if args.lockstep:
-            eng.rollout(kind, 1234, c, flags=flags, time_limits=limits)
+            eng.rollout(kind, 1234, c, flags=f, time_limits=limits)
         else:  # the same B x c decisions, claimed by whichever env is ready; preemptible at event boundaries
             pre = 0 if args.no_preempt else _abi.SSIM_ROLLOUT_PREEMPT
-            eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=flags | pre, time_limits=limits)
+            eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=f | pre, time_limits=limits)
 
     def run(n, events=None, chunk=None):
         """n steps; `events` (list of HIP event pairs) brackets each kernel launch on the launch stream."""
@@ -444,7 +446,7 @@ def main():
                 if events is not None:
                     e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     e[0].record(stream)
-                rollout_launch(c)
+                rollout_launch(c, events is not None)
                 if events is not None:
                     e[1].record(stream)
                     events.append(e)

@@ -9,6 +9,7 @@ NUM_ACC = 8  # int64 accumulators per env (ob_acc): S_act, E_act, J_act, events,
 ACC_NODES, ACC_EDGES, ACC_JOBS, ACC_EVENTS, ACC_DECISIONS, ACC_EPISODES = range(6)
 SSIM_ROLLOUT_AUTORESET = 0x1
 SSIM_ROLLOUT_PREEMPT = 0x2
+SSIM_ROLLOUT_WARMUP = 0x4
 SSIM_ERR_SPACE = 0x1
 SSIM_ERR_KEY = 0x2
 SSIM_ERR_TOO_MANY = 0x4

@@ -192,6 +192,9 @@ int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
  * the step stays pending (SSIM_ERR_PENDING) and the next launch on the handle completes it first. Decisions
  * are counted when they complete (ob_acc), so back-to-back launches count every decision exactly once. */
 #define SSIM_ROLLOUT_PREEMPT 0x2
+/* Same rollout, launched under the kernel symbol k_rollout_warmup instead of k_rollout, so a profiler's per-kernel
+ * statistics can tell launches that are not measured (a benchmark's pre-roll and warm-up) from measured ones. */
+#define SSIM_ROLLOUT_WARMUP 0x4
 int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
                     const double* time_limits, int32_t* action_log, void* stream);
 

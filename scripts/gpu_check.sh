@@ -35,6 +35,7 @@ for s in "$@"; do
     cpubase) step cpubase 900 python scripts/cpu_baselines.py ;;
     abargs)  step abargs 900 bash scripts/ab_args.sh ;;
     launch)  step launch 600 python scripts/launch_profile.py ;;
+    prof_driver) step prof_driver 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_driver" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 ;;
     ab20np)  step ab20np 900 env AB_TAG=s20np AB_ARGS="--steps 20 --warmup 5 --no-preempt" bash scripts/ab_tpch.sh ;;
     ab20)    step ab20 900 env AB_TAG=s20 AB_ARGS="--steps 20 --warmup 5" bash scripts/ab_tpch.sh ;;
     pmc)     step pmc 900 bash scripts/pmc_profile.sh ;;

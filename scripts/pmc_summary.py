@@ -82,6 +82,16 @@ def main():
             if cyc:
                 entry["wave_cycle_split"] = {k: w[k] / cyc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
                                                                      "SQ_ACTIVE_INST_ANY") if k in w}
+                # the bound that binds for one wave per SIMD: the fraction of the wave's life it
+                # spends issuing instructions (SQ_* wave counters count quad-cycles; ratios are unit-free)
+                pd = entry["per_decision"]
+                entry["issue"] = {
+                    "bound": "issue/latency: one wave per SIMD, one serial event chain per env",
+                    "frac": w["SQ_ACTIVE_INST_ANY"] / cyc, "wait_frac": w.get("SQ_WAIT_ANY", 0.0) / cyc,
+                    "wave_cycles_per_decision": 4.0 * pd["SQ_WAVE_CYCLES"],
+                    "instructions_per_decision": {k.replace("SQ_INSTS_", "").lower(): pd[k] for k in pd
+                                                  if k.startswith("SQ_INSTS_")},
+                    "simds": 1024}
         res["kernels"][kern] = entry
     txt = json.dumps(res, indent=1)
     if out:
