@@ -39,6 +39,13 @@
 #define SSIM_MARK(name) (void)0
 #endif
 
+// No floating-point contraction anywhere in the engine: the reference's float64 arithmetic rounds every product
+// before the add (e.g. job arrivals t += exponential(1 / rate) = t + round(scale * e), tpch.py:70), and a fused
+// multiply-add would change the last bit of the times the parity checks compare bit for bit.
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
 namespace ssim {
 
 // Dataset pointers are loaded from the Params block, so the compiler sees generic pointers and would emit

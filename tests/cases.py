@@ -267,6 +267,8 @@ def case_sampled_reset(make, dataset, env_cfg, cfg_over, B, seed0, mean_limit):
     host.reset(seeds=seeds, options=opts)
     dev.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=lim)
     assert np.array_equal(host.snapshot_obs(), dev.snapshot_obs()), "reset(seed) obs"
+    # every job's arrival time (t += exponential(1/rate), tpch.py:70: a rounded product, then the add)
+    assert np.array_equal(host.job_times_np()[0], dev.job_times_np()[0]), "job arrival times"
     for k in range(60):  # same actions on both
         si, ne = host.policy(_abi.SSIM_POLICY_FAIR)
         si, ne = np.array(host.to_numpy(si)), np.array(host.to_numpy(ne))
@@ -278,6 +280,7 @@ def case_sampled_reset(make, dataset, env_cfg, cfg_over, B, seed0, mean_limit):
     dev.reset_sampled(_abi.SSIM_RESET_CONTINUE, time_limits=lim2)
     a, b = host.snapshot_obs(), dev.snapshot_obs()
     assert np.array_equal(a, b), "reset(seed=None) obs"
+    assert np.array_equal(host.job_times_np()[0], dev.job_times_np()[0]), "job arrival times after reset(None)"
     v = dev.host_views()
     assert all(int(v["counts"][i][_abi.OC_EPISODE]) == 2 for i in range(B))
     assert all(int(v["counts"][i][_abi.OC_ERR]) == 0 for i in range(B))
