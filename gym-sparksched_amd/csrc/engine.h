@@ -901,12 +901,24 @@ struct Sim {
     if (s.sel) return false;
     if (s.rem - (s.mov + s.com) <= 0) return false;
     const int base = jr.base;
+    if (topo_masks()) {  // one dataset load for all parents, then their records
+      uint32_t pm = (uint32_t)ldg(D.ts_topo, s.ts);
+      while (pm) {
+        const StageRec ps = stage(base + __builtin_ctz(pm));
+        pm &= pm - 1;
+        if (ps.rem - (ps.mov + ps.com) > 0) return false;
+      }
+      return true;
+    }
     for (int k = ldg(D.ts_parent_base, s.ts); k < ldg(D.ts_parent_base, s.ts + 1); ++k) {
       const StageRec ps = stage(base + ldg(D.ts_parents, k));
       if (ps.rem - (ps.mov + ps.com) > 0) return false;
     }
     return true;
   }
+
+  // Templates of <= 32 stages: the DAG neighbourhood of a stage as bit sets (ssim_dataset.ts_topo)
+  __device__ __forceinline__ bool topo_masks() const { return C.max_stages <= 32 && D.ts_topo != nullptr; }
 
   // first schedulable stage in node order, or -1
   __device__ __forceinline__ int scan_first(int mode, int jx, int src_job) {
@@ -1156,6 +1168,16 @@ struct Sim {
     job_nact(j) -= 1;
     const int ts = st_ts(g), base = job_base(j);
     bool changed = false;
+    if (topo_masks()) {
+      uint32_t cm = (uint32_t)(ldu(D.ts_topo, ts) >> 32);
+      while (cm) {
+        const int c = base + __builtin_ctz(cm);
+        cm &= cm - 1;
+        st_unmet(c) -= 1;
+        if (st_unmet(c) == 0 && !st_completed(c)) changed = true;
+      }
+      return changed;
+    }
     const int kb = ldu(D.ts_child_base, ts), ke = ldu(D.ts_child_base, ts + 1);
     for (int k = kb; k < ke; ++k) {
       const int c = base + ldu(D.ts_children, k);
@@ -1428,27 +1450,49 @@ struct Sim {
       const bool ok = i < n;
       const int g = ok ? act[i] : -1;
       int cnt = 0, cb = 0, ce = 0, base = 0;
+      uint32_t live = 0;  // (bit-set path) the children that are not completed, ascending local id
       if (ok) {
         const StageRec sr = stage(g);
         base = job(sr.job).base;
-        cb = ldg(D.ts_child_base, sr.ts);
-        ce = ldg(D.ts_child_base, sr.ts + 1);
-        for (int k = cb; k < ce; ++k) {
-          const StageRec c = stage(base + ldg(D.ts_children, k));
-          if (!(c.rem == 0 && c.exe == 0)) cnt++;
+        if (topo_masks()) {
+          uint32_t cm = (uint32_t)(ldg(D.ts_topo, sr.ts) >> 32);
+          while (cm) {
+            const int b = __builtin_ctz(cm);
+            cm &= cm - 1;
+            const StageRec c = stage(base + b);
+            if (!(c.rem == 0 && c.exe == 0)) live |= 1u << b;
+          }
+          cnt = __builtin_popcount(live);
+        } else {
+          cb = ldg(D.ts_child_base, sr.ts);
+          ce = ldg(D.ts_child_base, sr.ts + 1);
+          for (int k = cb; k < ce; ++k) {
+            const StageRec c = stage(base + ldg(D.ts_children, k));
+            if (!(c.rem == 0 && c.exe == 0)) cnt++;
+          }
         }
       }
       int total = 0;
       const int ex = W::excl_scan(cnt, &total);
       if (ok) {
         int o = ne + ex;
-        for (int k = cb; k < ce; ++k) {
-          const int c = base + ldg(D.ts_children, k);
-          const StageRec cr = stage(c);
-          if (!(cr.rem == 0 && cr.exe == 0) && o < L.edge_cap) {
+        if (topo_masks()) {
+          while (live && o < L.edge_cap) {
+            const int c = base + __builtin_ctz(live);
+            live &= live - 1;
             links[2 * o + 0] = i;
             links[2 * o + 1] = row_of[c];
             o++;
+          }
+        } else {
+          for (int k = cb; k < ce; ++k) {
+            const int c = base + ldg(D.ts_children, k);
+            const StageRec cr = stage(c);
+            if (!(cr.rem == 0 && cr.exe == 0) && o < L.edge_cap) {
+              links[2 * o + 0] = i;
+              links[2 * o + 1] = row_of[c];
+              o++;
+            }
           }
         }
       }

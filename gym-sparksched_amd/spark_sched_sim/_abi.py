@@ -69,13 +69,14 @@ class SsimDataset(ct.Structure):
         ("dur_len", ct.c_void_p),
         ("durations", ct.c_void_p),
         ("intervals", ct.c_void_p),
+        ("ts_topo", ct.c_void_p),
     ]
 
 
 # order of the pointer fields above = order of arrays in PackedDataset.arrays()
 DATASET_ARRAYS = [
     "tpl_stage_base", "ts_num_tasks", "ts_rough", "ts_child_base", "ts_children", "ts_parent_base",
-    "ts_parents", "ts_fw_keymask", "ts_fw_maxlevel", "dur_off", "dur_len", "durations", "intervals",
+    "ts_parents", "ts_fw_keymask", "ts_fw_maxlevel", "dur_off", "dur_len", "durations", "intervals", "ts_topo",
 ]
 
 

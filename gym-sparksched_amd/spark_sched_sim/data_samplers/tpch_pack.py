@@ -77,6 +77,7 @@ class PackedDataset:
     dur_len: np.ndarray
     durations: np.ndarray
     intervals: np.ndarray
+    ts_topo: np.ndarray  # uint64 [TS]: parent bits 0-31, child bits 32-63 (zeros if a template has > 32 stages)
 
     def arrays(self) -> list[np.ndarray]:
         from .._abi import DATASET_ARRAYS
@@ -101,6 +102,7 @@ def pack(raw: dict, num_executors: int) -> PackedDataset:
     num_tasks, rough, keymask, maxlevel = [], [], [], []
     child_base, children, parent_base, parents = [0], [], [0], []
     dur_off, dur_len, durations = [], [], []
+    topo = []
     max_stages = max_edges = 0
     for tid in range(n_tpl):
         q, si = tid // len(QUERY_SIZES) + 1, tid % len(QUERY_SIZES)
@@ -142,6 +144,10 @@ def pack(raw: dict, num_executors: int) -> PackedDataset:
             child_base.append(len(children))
             parents.extend(pars[sid])
             parent_base.append(len(parents))
+            if n <= 32:
+                topo.append(sum(1 << p for p in pars[sid]) | (sum(1 << c for c in kids[sid]) << 32))
+            else:
+                topo.append(0)
         stage_base.append(stage_base[-1] + n)
     i32 = lambda x: np.ascontiguousarray(np.asarray(x, dtype=np.int32))  # noqa: E731
     return PackedDataset(
@@ -162,4 +168,5 @@ def pack(raw: dict, num_executors: int) -> PackedDataset:
         dur_len=i32(dur_len),
         durations=np.ascontiguousarray(np.asarray(durations if durations else [0.0], dtype=np.float64)),
         intervals=np.ascontiguousarray(executor_intervals(num_executors).reshape(-1)),
+        ts_topo=np.ascontiguousarray(np.asarray(topo if max_stages <= 32 else [0] * len(topo), dtype=np.uint64)),
     )

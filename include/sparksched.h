@@ -82,6 +82,10 @@ typedef struct ssim_dataset {
   const int32_t* dur_len;         /* [TS*3*8] */
   const double* durations;
   const double* intervals;        /* [(N+1)*2] executor_intervals (tpch.py:237-262) */
+  const uint64_t* ts_topo;        /* [TS] the same DAG as bit sets of local stage ids when every template has
+                                     <= 32 stages (config max_stages <= 32): parents in bits 0-31, children in bits
+                                     32-63; one load gives a stage's whole neighbourhood (the CSR takes a chain of
+                                     dependent loads). Ignored for max_stages > 32. */
 } ssim_dataset;
 
 /* Per-env reset record (host-sampled job sequence; spark_sched_sim.py:127-186 / tpch.py:54-73).

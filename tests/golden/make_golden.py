@@ -58,10 +58,17 @@ def trace_digest(trace) -> str:
     return h.hexdigest()
 
 
+# the packed arrays the digest pins (the generator's output as the device sees it; arrays derived from these
+# later, e.g. ts_topo from the parent / child CSR, are not part of the pin)
+DIGEST_ARRAYS = ["tpl_stage_base", "ts_num_tasks", "ts_rough", "ts_child_base", "ts_children", "ts_parent_base",
+                 "ts_parents", "ts_fw_keymask", "ts_fw_maxlevel", "dur_off", "dur_len", "durations", "intervals"]
+
+
 def dataset_digest(ds) -> str:
     h = hashlib.sha256()
-    for a in pack(ds, 10).arrays():
-        h.update(np.ascontiguousarray(a).tobytes())
+    p = pack(ds, 10)
+    for name in DIGEST_ARRAYS:
+        h.update(np.ascontiguousarray(getattr(p, name)).tobytes())
     return h.hexdigest()
 
 

@@ -115,3 +115,17 @@ def test_layout_structs_match_header():
     assert len(SsimDataset._fields_) == 2 + len(DATASET_ARRAYS)
     cfg.num_executors = 0
     assert lib.ssim_layout_for(ctypes.byref(cfg), ctypes.byref(L)) != 0
+
+
+def test_topology_bit_sets_match_csr(dataset):
+    """ts_topo (parents in bits 0-31, children in bits 32-63 of each template stage) holds exactly the CSR's DAG."""
+    from spark_sched_sim.data_samplers.tpch_pack import pack
+
+    p = pack(dataset, 10)
+    assert p.max_stages <= 32 and p.ts_topo.dtype == np.uint64 and p.ts_topo.shape == (p.num_template_stages,)
+    for ts in range(p.num_template_stages):
+        par = p.ts_parents[p.ts_parent_base[ts]: p.ts_parent_base[ts + 1]]
+        kid = p.ts_children[p.ts_child_base[ts]: p.ts_child_base[ts + 1]]
+        w = int(p.ts_topo[ts])
+        assert [b for b in range(32) if (w >> b) & 1] == sorted(par.tolist())
+        assert [b for b in range(32) if (w >> (32 + b)) & 1] == kid.tolist()  # CSR children are ascending
