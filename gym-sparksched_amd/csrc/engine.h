@@ -110,13 +110,13 @@ struct Params {
   uint8_t iv[kIvRows][4];
 };
 constexpr int64_t kParamsReserve = 4096;
-// The last 1 KB of the params block holds the shared-budget rollouts' decision counters (ssim_rollout_budget):
-// two slots used alternately, each with kTicketShards counters on separate 64-B lines (one per XCD group of envs,
-// env e -> shard e % kTicketShards, the round-robin workgroup-to-XCD dispatch order).
-constexpr int kTicketShards = 8;
-constexpr int64_t kTicketOffset = kParamsReserve - 1024;
+// The last 2 KB of the params block hold the shared-budget rollouts' state (ssim_rollout_budget): two slots used
+// alternately, each one 64-B line for the decision counter followed by kStopLines lines of the "budget spent" flag
+// (env e polls line e % kStopLines, one per XCD under round-robin workgroup dispatch).
+constexpr int kStopLines = 8;
+constexpr int64_t kTicketOffset = kParamsReserve - 2048;
 constexpr int64_t kTicketStride = 64;
-constexpr int64_t kTicketSlotBytes = kTicketShards * kTicketStride;
+constexpr int64_t kTicketSlotBytes = (1 + kStopLines) * kTicketStride;
 static_assert(sizeof(Params) <= kTicketOffset, "params block");
 
 __host__ __device__ inline int exec_level_index(double key) {  // EXEC_LEVELS index, 0xFF if not a level

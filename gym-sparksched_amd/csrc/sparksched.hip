@@ -66,17 +66,37 @@ __global__ __launch_bounds__(64) void k_reset_sampled(const Params* __restrict__
 #endif
 constexpr int32_t kFlagTicketSlot = 0x100;  // internal k_rollout flag: use the second budget counter
 
-// The preemptible budget rollout's stop condition: the shared decision counter has reached the budget. The load is
-// issued one event ahead of its test (Sim::simulate), so its latency hides behind that event's handling.
+// The budget rollout's decision counter and "budget spent" flag. Claims take chunks of decisions from one atomic
+// counter (tens of claims per microsecond over the whole chip); the wave whose claim finds the budget spent raises
+// the flag on kStopLines lines, and with SSIM_ROLLOUT_PREEMPT every running step polls its own line
+// (env % kStopLines) every few events, so the polls spread over eight lines instead of queueing on the counter.
+// `issue` starts a poll one event before `hit` tests it (Sim::simulate), hiding its latency.
 struct TicketStop {
   static constexpr bool kCan = true;
-  const unsigned long long* p;
-  int64_t budget;
-  bool on;
-  __device__ __forceinline__ uint64_t issue() const {
-    return on ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  uint8_t* base;   // this launch's slot (null: no budget)
+  int64_t total;   // the launch's budget
+  int line;        // this wave's flag line
+  bool on;         // preemption enabled
+  __device__ __forceinline__ unsigned long long* word(int l) const {
+    return reinterpret_cast<unsigned long long*>(base + kTicketStride * l);
   }
-  __device__ __forceinline__ bool hit(uint64_t v) const { return on && (int64_t)WaveHip::uni(v) >= budget; }
+  // Decisions granted to this wave (0: the budget is spent). The chunk follows what is left per env: 8 early,
+  // 1 at the end (guided self-scheduling). `last` = the counter at this wave's previous claim.
+  __device__ __forceinline__ int64_t claim(int64_t num_envs, int64_t& last) const {
+    int64_t c = (total - last) / (4 * num_envs);
+    c = c < 1 ? 1 : c > 8 ? 8 : c;
+    unsigned long long t = 0;
+    if (WaveHip::lane() == 0) t = atomicAdd(word(0), (unsigned long long)c);
+    last = (int64_t)WaveHip::uni((uint64_t)t);
+    if (last < total) return total - last < c ? total - last : c;
+    if (WaveHip::lane() < kStopLines)  // the budget is spent: stop the steps still simulating
+      __hip_atomic_store(word(1 + WaveHip::lane()), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  __device__ __forceinline__ uint64_t issue() const {
+    return on ? __hip_atomic_load(word(1 + line), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  }
+  __device__ __forceinline__ bool hit(uint64_t v) const { return on && WaveHip::uni(v) != 0; }
 };
 
 template <bool kRes, int kN, int kJ, int kS>
@@ -120,7 +140,7 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
                                                 const int32_t* __restrict__ env_steps) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
-  if (budget > 0 && eid == 0 && WaveHip::lane() < kTicketShards)  // the next budget launch's counters (`tickets`)
+  if (budget > 0 && eid == 0 && WaveHip::lane() <= kStopLines)  // the next budget launch's slot (TicketStop)
     *reinterpret_cast<unsigned long long*>(state + kTicketOffset + ((flags & kFlagTicketSlot) ? 0 : kTicketSlotBytes) +
                                            kTicketStride * WaveHip::lane()) = 0ull;
   if (env_steps != nullptr) {  // per-env decision counts (ssim_rollout_steps), capped by num_steps
@@ -144,23 +164,12 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
   // budget running out instead of waiting for the env with the most expensive K decisions. With
   // SSIM_ROLLOUT_PREEMPT it ends within ~one EVENT: a step still simulating when the budget runs out stops at
   // its next event boundary and stays pending for the next launch.
-  // Two counter slots used alternately (kFlagTicketSlot): this launch's start at 0 because the previous budget
-  // launch zeroed them, and this launch zeroes the other slot for the next (launches on a stream are ordered), so
-  // no memset launch precedes a budget launch. The budget is split over kTicketShards counters (env e claims from
-  // shard e % kTicketShards, its XCD under round-robin dispatch), so claims and the preemption polls spread over
-  // eight cache lines instead of queueing on one atomic word; each shard spends its share exactly.
+  // Two slots used alternately (kFlagTicketSlot): this launch's starts zeroed because the previous budget launch
+  // zeroed it, and this launch zeroes the other for the next (launches on a stream are ordered), so no memset
+  // launch precedes a budget launch.
   const int slot = (flags & kFlagTicketSlot) ? 1 : 0;
-  const int shard = eid % kTicketShards;
-  const int nshard = B < kTicketShards ? B : kTicketShards;
-  const int shard_envs = B / nshard + (shard < B % nshard ? 1 : 0);
-  const bool budgeted = budget > 0;
-  if (budgeted) budget = budget / nshard + (shard < budget % nshard ? 1 : 0);  // this shard's share (may be 0)
-  unsigned long long* tickets =
-      budgeted ? reinterpret_cast<unsigned long long*>(state + kTicketOffset + kTicketSlotBytes * slot +
-                                                       kTicketStride * shard)
-               : nullptr;
-
-  const TicketStop stop{tickets, budget, tickets != nullptr && (flags & SSIM_ROLLOUT_PREEMPT) != 0};
+  const TicketStop stop{budget > 0 ? state + kTicketOffset + kTicketSlotBytes * slot : nullptr, budget,
+                        eid % kStopLines, budget > 0 && (flags & SSIM_ROLLOUT_PREEMPT) != 0};
   int64_t granted = 0, last = 0;
   // One loop both starts steps and completes a step a previous launch preempted (pending), so the simulation /
   // observation code (finish_step) is inlined once.
@@ -176,17 +185,9 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
       simulate = true;
     } else {
       if (k >= num_steps) break;
-      if (tickets != nullptr) {
+      if (stop.base != nullptr) {
         if (!autoreset && (s.h.terminated || s.frozen())) break;
-        if (granted == 0) {
-          int64_t c = (budget - last) / (4 * (int64_t)shard_envs);
-          c = c < 1 ? 1 : c > 8 ? 8 : c;
-          unsigned long long t = 0;
-          if (WaveHip::lane() == 0) t = atomicAdd(tickets, (unsigned long long)c);
-          last = (int64_t)WaveHip::uni((uint64_t)t);
-          if (last >= budget) break;
-          granted = budget - last < c ? budget - last : c;
-        }
+        if (granted == 0 && (granted = stop.claim(B, last)) == 0) break;
         --granted;
       }
       const StepIn a = sim_policy(s, kind, seed);
@@ -380,6 +381,8 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
     }
   }
   int rc = hip_check(hipMemcpy(h->state, &h->params, sizeof(Params), hipMemcpyHostToDevice), "params upload");
+  if (rc == SSIM_OK)  // both budget slots start zeroed (each budget launch then zeroes the other, TicketStop)
+    rc = hip_check(hipMemset(h->state + kTicketOffset, 0, (size_t)(2 * kTicketSlotBytes)), "budget slots clear");
   if (rc == SSIM_OK) rc = hip_check(hipMemset(h->obs, 0, (size_t)h->params.L.obs_bytes), "obs clear");
   if (rc == SSIM_OK)
     rc = hip_check(hipMemset(h->state + kParamsReserve, 0, (size_t)(h->params.L.state_bytes - kParamsReserve)),
