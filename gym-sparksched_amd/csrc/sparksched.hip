@@ -12,24 +12,11 @@
 #include <stdio.h>
 #include <string.h>
 
-#include "sparksched.h"
-#include "engine.h"
+#include "kernels.h"
 #include "decima.h"
 #include "decima_policy.h"
-#include "policy.h"
-#include "wave_hip.h"
-
-using namespace ssim;
 
 // ------------------------------------------------------------------------------------------ kernels
-extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
-
-// An env whose header says terminated / frozen / never reset is skipped without touching LDS.
-__device__ __forceinline__ bool env_idle(const Params* __restrict__ P, const uint8_t* state, int eid) {
-  const EnvHeader* gh =
-      reinterpret_cast<const EnvHeader*>(state + kParamsReserve + (int64_t)eid * P->L.env_bytes + P->O.hdr);
-  return gh->terminated || (gh->err & SSIM_ERR_STICKY) || gh->num_jobs == 0;
-}
 
 __global__ __launch_bounds__(64) void k_reset(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                               const uint8_t* __restrict__ reset) {
@@ -52,74 +39,6 @@ __global__ __launch_bounds__(64) void k_reset_sampled(const Params* __restrict__
                   reset + (int64_t)eid * P->L.reset_stride);
 }
 
-// kRes: hot block LDS-resident. A compile-time flag (not a runtime select between an LDS and an HBM pointer)
-// so every hot-block access compiles to ds_read/ds_write rather than FLAT instructions.
-// Waves per SIMD the HBM-resident (kRes = false) kernels are compiled for. Their state lives in HBM, so the
-// event loop is bound by memory latency and occupancy hides it; the LDS-resident ones run one wave per SIMD
-// by LDS budget anyway. Register caps: 2 waves -> 256 VGPRs, 4 -> 128. Measured on the configs[3] shard (4096
-// envs, J=200, N=100): 8.9M decisions/s at 1 wave (266 VGPRs), 15.2M at 2, 17.3M at 4 (despite scratch spills).
-#ifndef SSIM_HBM_ROLLOUT_WAVES
-#define SSIM_HBM_ROLLOUT_WAVES 4
-#endif
-#ifndef SSIM_HBM_STEP_WAVES
-#define SSIM_HBM_STEP_WAVES 4
-#endif
-constexpr int32_t kFlagTicketSlot = 0x100;  // internal k_rollout flag: use the second budget counter
-
-// The budget rollout's decision counter and "budget spent" flag. Claims take chunks of decisions from one atomic
-// counter (tens of claims per microsecond over the whole chip); the wave whose claim finds the budget spent raises
-// the flag on kStopLines lines, and with SSIM_ROLLOUT_PREEMPT every running step polls its own line
-// (env % kStopLines) every few events, so the polls spread over eight lines instead of queueing on the counter.
-// `issue` starts a poll one event before `hit` tests it (Sim::simulate), hiding its latency.
-struct TicketStop {
-  static constexpr bool kCan = true;
-  uint8_t* base;   // this launch's slot (null: no budget)
-  int64_t total;   // the launch's budget
-  int line;        // this wave's flag line
-  bool on;         // preemption enabled
-  __device__ __forceinline__ unsigned long long* word(int l) const {
-    return reinterpret_cast<unsigned long long*>(base + kTicketStride * l);
-  }
-  // Decisions granted to this wave (0: the budget is spent). The chunk follows what is left per env: 8 early,
-  // 1 at the end (guided self-scheduling). `last` = the counter at this wave's previous claim.
-  __device__ __forceinline__ int64_t claim(int64_t num_envs, int64_t& last) const {
-    int64_t c = (total - last) / (4 * num_envs);
-    c = c < 1 ? 1 : c > 8 ? 8 : c;
-    unsigned long long t = 0;
-    if (WaveHip::lane() == 0) t = atomicAdd(word(0), (unsigned long long)c);
-    last = (int64_t)WaveHip::uni((uint64_t)t);
-    if (last < total) return total - last < c ? total - last : c;
-    if (WaveHip::lane() < kStopLines)  // the budget is spent: stop the steps still simulating
-      __hip_atomic_store(word(1 + WaveHip::lane()), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return 0;
-  }
-  __device__ __forceinline__ uint64_t issue() const {
-    return on ? __hip_atomic_load(word(1 + line), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-  }
-  __device__ __forceinline__ bool hit(uint64_t v) const { return on && WaveHip::uni(v) != 0; }
-};
-
-template <bool kRes, int kN, int kJ, int kS>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_STEP_WAVES))) void k_step(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
-                                             const int32_t* __restrict__ stage_idx,
-                                             const int32_t* __restrict__ num_exec) {
-  const int eid = blockIdx.x;
-  if (env_idle(P, state, eid)) return;
-  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
-  StepIn a;
-  a.stage_idx = stage_idx[eid];
-  a.num_exec = num_exec[eid];
-  s.load_hot();
-  s.load_header();
-  if (s.pending()) {  // a preempted step completes first; this call's action (chosen on a stale obs) is dropped
-    s.resume(NoStop());
-    s.write_err_only(SSIM_ERR_PENDING);
-  } else {
-    s.step_loaded(a);
-  }
-  s.save_hot();
-}
-
 __global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, const uint8_t* obs, int kind,
                                                uint64_t seed, uint64_t counter, int32_t* stage_idx,
                                                int32_t* num_exec) {
@@ -130,119 +49,6 @@ __global__ __launch_bounds__(64) void k_policy(const Params* __restrict__ P, con
     stage_idx[eid] = a.stage_idx;
     num_exec[eid] = a.num_exec;
   }
-}
-
-template <bool kRes, int kN, int kJ, int kS>
-__device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
-                                                int kind, uint64_t seed, int num_steps, int flags,
-                                                const double* __restrict__ limits, uint8_t* reset,
-                                                int32_t* action_log, uint64_t* prof_out, int64_t budget,
-                                                const int32_t* __restrict__ env_steps) {
-  const int eid = blockIdx.x;
-  const int B = P->L.num_envs;
-  if (budget > 0 && eid == 0 && WaveHip::lane() <= kStopLines)  // the next budget launch's slot (TicketStop)
-    *reinterpret_cast<unsigned long long*>(state + kTicketOffset + ((flags & kFlagTicketSlot) ? 0 : kTicketSlotBytes) +
-                                           kTicketStride * WaveHip::lane()) = 0ull;
-  if (env_steps != nullptr) {  // per-env decision counts (ssim_rollout_steps), capped by num_steps
-    const int n = env_steps[eid];
-    num_steps = n < num_steps ? n : num_steps;
-    if (num_steps <= 0) return;
-  }
-  const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
-  if (env_idle(P, state, eid) && action_log == nullptr && !autoreset) return;
-#ifdef SSIM_PROFILE
-  const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime();
-#endif
-  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
-  s.load_hot();
-#ifdef SSIM_PROFILE
-  s.prof[kTEntry] = rt_entry;
-  s.prof[kTLoaded] = __builtin_amdgcn_s_memrealtime();
-#endif
-  // Shared budget (budget > 0): decisions are claimed from one device counter in chunks sized to what is
-  // left (guided self-scheduling: 8 early, 1 at the end), so the launch ends within ~one decision of the
-  // budget running out instead of waiting for the env with the most expensive K decisions. With
-  // SSIM_ROLLOUT_PREEMPT it ends within ~one EVENT: a step still simulating when the budget runs out stops at
-  // its next event boundary and stays pending for the next launch.
-  // Two slots used alternately (kFlagTicketSlot): this launch's starts zeroed because the previous budget launch
-  // zeroed it, and this launch zeroes the other for the next (launches on a stream are ordered), so no memset
-  // launch precedes a budget launch.
-  const int slot = (flags & kFlagTicketSlot) ? 1 : 0;
-  const TicketStop stop{budget > 0 ? state + kTicketOffset + kTicketSlotBytes * slot : nullptr, budget,
-                        eid % kStopLines, budget > 0 && (flags & SSIM_ROLLOUT_PREEMPT) != 0};
-  int64_t granted = 0, last = 0;
-  // One loop both starts steps and completes a step a previous launch preempted (pending), so the simulation /
-  // observation code (finish_step) is inlined once.
-  for (int k = 0;;) {
-#ifdef SSIM_PROFILE
-    const uint64_t t0 = WaveHip::clock();
-#endif
-    s.load_header();
-    double st0 = 0.0;
-    bool simulate;
-    if (s.pending()) {  // completes first, whatever this launch's mode; not one of its num_steps
-      st0 = s.take_pending();
-      simulate = true;
-    } else {
-      if (k >= num_steps) break;
-      if (stop.base != nullptr) {
-        if (!autoreset && (s.h.terminated || s.frozen())) break;
-        if (granted == 0 && (granted = stop.claim(B, last)) == 0) break;
-        --granted;
-      }
-      const StepIn a = sim_policy(s, kind, seed);
-#ifdef SSIM_PROFILE
-      s.prof[kPhPolicy] += WaveHip::clock() - t0;
-#endif
-      if (action_log != nullptr && WaveHip::lane() == 0) {
-        action_log[((int64_t)k * B + eid) * 2 + 0] = a.stage_idx;
-        action_log[((int64_t)k * B + eid) * 2 + 1] = a.num_exec;
-      }
-      ++k;
-      WaveHip::sync();
-      simulate = s.step_begin(a, &st0);
-    }
-    if (simulate && !s.finish_step(st0, stop)) break;  // preempted mid-simulation: pending until the next launch
-    // episode over (terminated, or truncated by the time limit): reset(seed=None) in place
-    if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit))
-      s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
-                      reset + (int64_t)eid * P->L.reset_stride);
-#ifdef SSIM_PROFILE
-    {
-      const uint64_t dc = WaveHip::clock() - t0;
-      int b = 63 - __builtin_clzll(dc | 1ull) - 10;
-      b = b < 0 ? 0 : b > 15 ? 15 : b;
-      s.prof[kHist0 + b] += 1;
-    }
-#endif
-  }
-#ifdef SSIM_PROFILE
-  s.prof[kTLoopEnd] = __builtin_amdgcn_s_memrealtime();
-#endif
-  s.save_hot();
-#ifdef SSIM_PROFILE
-  s.prof[kTSaved] = __builtin_amdgcn_s_memrealtime();
-  if (prof_out != nullptr && WaveHip::lane() == 0)
-    for (int p = 0; p < kNumPhases; ++p) prof_out[(int64_t)eid * kNumPhases + p] = s.prof[p];
-#else
-  (void)prof_out;
-#endif
-}
-
-#define SSIM_ROLLOUT_ARGS                                                                                       \
-  const Params *__restrict__ P, uint8_t *state, uint8_t *obs, int kind, uint64_t seed, int num_steps, int flags, \
-      const double *__restrict__ limits, uint8_t *reset, int32_t *action_log, uint64_t *prof_out, int64_t budget, \
-      const int32_t *__restrict__ env_steps
-#define SSIM_ROLLOUT_PASS P, state, obs, kind, seed, num_steps, flags, limits, reset, action_log, prof_out, budget, env_steps
-template <bool kRes, int kN, int kJ, int kS>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_ROLLOUT_WAVES))) void k_rollout(SSIM_ROLLOUT_ARGS) {
-  rollout_body<kRes, kN, kJ, kS>(SSIM_ROLLOUT_PASS);
-}
-// The same rollout under its own symbol for launches that are not measured (SSIM_ROLLOUT_WARMUP: a benchmark's
-// pre-roll and warm-up), so a profiler's per-kernel statistics of k_rollout cover the timed launches only.
-template <bool kRes, int kN, int kJ, int kS>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_ROLLOUT_WAVES))) void k_rollout_warmup(SSIM_ROLLOUT_ARGS) {
-  rollout_body<kRes, kN, kJ, kS>(SSIM_ROLLOUT_PASS);
 }
 
 __global__ __launch_bounds__(64) void k_decima(const Params* __restrict__ P, const uint8_t* obs, float nts,
@@ -294,22 +100,16 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
 // 10 executors, 50 jobs): fully (stage cap too) when the packed dataset's cap is the synthetic set's 50 x 18, else
 // on (executors, jobs) with the stage cap read at run time (any other TPC-H-format dataset, e.g. the real traces
 // loaded from data/tpch); other shapes use the generic instantiations.
-using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
-using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int, const double*, uint8_t*,
-                          int32_t*, uint64_t*, int64_t, const int32_t*);
 static bool bench_shape(const Params& p) { return p.L.num_executors == 10 && p.L.job_cap == 50; }
-static StepFn pick_step(const Params& p) {
-  if (!p.O.lds_resident) return k_step<false, 0, 0, 0>;
-  if (bench_shape(p)) return p.L.stage_cap == 900 ? k_step<true, 10, 50, 900> : k_step<true, 10, 50, 0>;
-  return k_step<true, 0, 0, 0>;
+static KernelSet pick_kernels(const Params& p) {
+  if (!p.O.lds_resident) return kernels_hbm();
+  if (bench_shape(p)) return p.L.stage_cap == 900 ? kernels_bench900() : kernels_bench();
+  return kernels_lds();
 }
+static StepFn pick_step(const Params& p) { return pick_kernels(p).step; }
 static RolloutFn pick_rollout(const Params& p, bool warmup = false) {
-  if (!p.O.lds_resident) return k_rollout<false, 0, 0, 0>;
-  if (bench_shape(p)) {
-    if (p.L.stage_cap == 900) return warmup ? k_rollout_warmup<true, 10, 50, 900> : k_rollout<true, 10, 50, 900>;
-    return warmup ? k_rollout_warmup<true, 10, 50, 0> : k_rollout<true, 10, 50, 0>;
-  }
-  return k_rollout<true, 0, 0, 0>;  // (warm-up launches of other shapes use the same symbol)
+  const KernelSet k = pick_kernels(p);
+  return warmup ? k.rollout_warmup : k.rollout;
 }
 
 // ------------------------------------------------------------------------------------------ C ABI

@@ -24,13 +24,11 @@ TOP = 8  # the first TOP phases are disjoint; the rest are inclusive sub-timers
 
 def build_prof():
     out = os.path.join(REPO, "gym-sparksched_amd", "build", "libsparksched_prof.so")
-    csrc = os.path.join(REPO, "gym-sparksched_amd", "csrc")
-    srcs = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(REPO, "include", "sparksched.h")]
-    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(f) for f in srcs):
+    if os.path.exists(out) and "--build" not in sys.argv:
         return out  # prebuilt in-tree (build on the CPU container: `python scripts/phase_profile.py --build`)
-    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DSSIM_PROFILE",
-                    f"-I{REPO}/include", f"-I{csrc}", os.path.join(csrc, "sparksched.hip"), "-o", out], check=True)
-    return out
+    import __graft_entry__
+
+    return __graft_entry__.build_lib(force=True, out=out, defines=["-DSSIM_PROFILE"])
 
 
 def main():

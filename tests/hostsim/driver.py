@@ -29,13 +29,25 @@ _lib = None
 
 
 def build(force: bool = False, extra_flags=()) -> str:
-    newest = max(os.path.getmtime(p) for p in SOURCES)
-    if force or not os.path.exists(SO_PATH) or os.path.getmtime(SO_PATH) < newest:
-        cmd = ["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
-               f"-I{os.path.join(REPO, 'include')}", f"-I{os.path.join(REPO, 'gym-sparksched_amd', 'csrc')}",
-               SOURCES[0], "-o", SO_PATH + ".tmp", *extra_flags]
-        subprocess.run(cmd, check=True)
-        os.replace(SO_PATH + ".tmp", SO_PATH)
+    """Builds _hostsim.so if stale. Safe under parallel test workers (pytest -n): one builder at a time holds
+    an flock, and each writes its own temporary before the atomic rename."""
+    import fcntl
+
+    def stale():
+        newest = max(os.path.getmtime(p) for p in SOURCES)
+        return not os.path.exists(SO_PATH) or os.path.getmtime(SO_PATH) < newest
+
+    if not force and not stale():
+        return SO_PATH
+    with open(SO_PATH + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if force or stale():
+            tmp = f"{SO_PATH}.{os.getpid()}.tmp"
+            cmd = ["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+                   "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}",
+                   f"-I{os.path.join(REPO, 'gym-sparksched_amd', 'csrc')}", SOURCES[0], "-o", tmp, *extra_flags]
+            subprocess.run(cmd, check=True)
+            os.replace(tmp, SO_PATH)
     return SO_PATH
 
 
