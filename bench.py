@@ -308,6 +308,12 @@ def run_ppo(args, rank, world, local, dev):
             "decisions": int(dec), "seconds_per_iteration": elapsed / args.steps,
             "phase_seconds_rank0": phases, "last_learning_stats": learn,
             "roofline": None, "cpu_baseline": None}
+        if not args.no_cpu_baseline and world == 1:
+            # the reference iteration's rollout phase: num_sequences x num_rollouts = 16 rollout processes
+            # (trainer.py:264-296) running the Decima GNN on the CPU; an upper bound on its decisions/s (the
+            # learner's time is excluded)
+            line["cpu_baseline"] = cpu_baseline("decima", args.cpu_seconds, B)
+            line["cpu_baseline"]["sample"] += "; rollout phase of the PPO iteration only (learner excluded)"
     return line
 
 

@@ -177,21 +177,111 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- hot-block residency
-  __device__ __forceinline__ void copy16(uint8_t* dst, const uint8_t* src, int64_t bytes) {
+  // LDS residency copies only the LIVE part of the hot block: the fixed sections (header, jobs, executors,
+  // commitments, the COMMON and job pools) and, of the per-stage sections, the stage and stage-pool records of
+  // the jobs from the lowest active one to the last arrived one plus the used prefix of the active-stage and
+  // schedulable lists. Stages of completed jobs are never read again and those of jobs not yet arrived are
+  // initialised at arrival (on_job_arrival), so nothing outside the range is read during the launch.
+  // A copy issues up to kCopyBatch 16-B loads per lane before any store (one memory latency per batch).
+  static constexpr int kCopyBatch = 12;
+  struct Span {
+    int64_t off, n;  // byte offset in the hot block, 16-B units
+  };
+  template <int kSpans>
+  __device__ __forceinline__ void copy_spans(uint8_t* dst, const uint8_t* src, const Span (&sp)[kSpans]) {
     W::sync();
-    const int64_t n = bytes >> 4;
-    for (int64_t i = W::lane(); i < n; i += W::kWidth)
-      reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    int64_t end[kSpans];
+    int64_t total = 0;
+#pragma unroll
+    for (int r = 0; r < kSpans; ++r) end[r] = (total += sp[r].n);
+    for (int64_t i0 = 0; i0 < total; i0 += (int64_t)W::kWidth * kCopyBatch) {
+      uint4 v[kCopyBatch];
+      int64_t at[kCopyBatch];
+#pragma unroll
+      for (int u = 0; u < kCopyBatch; ++u) {
+        const int64_t i = i0 + (int64_t)u * W::kWidth + W::lane();
+        int64_t o = -1;
+#pragma unroll
+        for (int r = kSpans - 1; r >= 0; --r)
+          if (i < end[r]) o = sp[r].off + ((i - (end[r] - sp[r].n)) << 4);
+        at[u] = i < total ? o : -1;
+        if (at[u] >= 0) v[u] = *reinterpret_cast<const uint4*>(src + at[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kCopyBatch; ++u)
+        if (at[u] >= 0) *reinterpret_cast<uint4*>(dst + at[u]) = v[u];
+    }
     W::sync();
   }
+  int32_t live_lo = 0;  // first stage of the live range (set by load_hot; 0 after an in-launch reset)
+  // End of the live stage range: the stages of every arrived job (hot block in place).
+  __device__ __forceinline__ int live_hi() const {
+    const int a = h.arrivals;
+    return a > 0 ? (int)job_base(a - 1) + (int)job_nst(a - 1) : 0;
+  }
+  __device__ __forceinline__ Span stage_span(int lo, int hi) const { return {O.stages + 16 * (int64_t)lo, hi - lo}; }
+  __device__ __forceinline__ Span pool_span(int lo, int hi) const {
+    return {O.pools + 16 * (int64_t)(1 + JC + lo), hi - lo};
+  }
+  __device__ __forceinline__ Span list_span(int64_t off, int n) const { return {off, (2 * (int64_t)n + 15) >> 4}; }
   __device__ __forceinline__ void load_hot() {
     SSIM_TIC(t0);
-    if (hot != ghot) copy16(hot, ghot, O.hot_bytes);
+    if (hot != ghot) {
+      const Span fixed[2] = {{0, O.stages >> 4}, {O.pools, 1 + JC}};
+      copy_spans(hot, ghot, fixed);
+      load_header();
+      // lowest stage still referenced (jobs' stages are contiguous in arrival order): the stages of the active
+      // jobs, and stage pools / stages a completed job can still be named by — an executor left in one of its
+      // stage pools (ex.loc), an executor moving to one of its stages (EXECUTOR_READY ev_stage), a commitment
+      // from or to one of its stage pools, the current source pool
+      const int16_t* aj = H<int16_t>(O.active_jobs);
+      constexpr int kNone = 0x7FFFFFFF;
+      int lo = is_stage_pool(h.source) ? pool_stage(h.source) : kNone;
+      for (int k0 = 0; k0 < h.n_active_jobs; k0 += W::kWidth) {
+        const int k = k0 + W::lane();
+        const int b = k < h.n_active_jobs ? (int)job(aj[k]).base : kNone;
+        lo = W::min_i(b < lo ? b : lo);
+      }
+      for (int k0 = 0; k0 < NE; k0 += W::kWidth) {
+        const int e = k0 + W::lane();
+        int b = kNone;
+        if (e < NE) {
+          const ExecRec x = exr(e);
+          if (is_stage_pool(x.loc)) b = pool_stage(x.loc);
+          if (x.ev_seq >= 0 && x.ev_stage >= 0 && x.ev_stage < b) b = x.ev_stage;
+        }
+        lo = W::min_i(b < lo ? b : lo);
+      }
+      for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
+        const int k = k0 + W::lane();
+        int b = kNone;
+        if (k < commit_cap_for(NE)) {
+          const CommitRec r = cm(k);
+          if (r.cnt > 0) {
+            if (is_stage_pool(r.src)) b = pool_stage(r.src);
+            if (is_stage_pool(r.dst) && pool_stage(r.dst) < b) b = pool_stage(r.dst);
+          }
+        }
+        lo = W::min_i(b < lo ? b : lo);
+      }
+      const int hi = live_hi();
+      live_lo = lo < hi ? lo : hi;
+      const Span live[4] = {stage_span(live_lo, hi), pool_span(live_lo, hi), list_span(O.active_stages, h.n_active_stages),
+                            list_span(O.sched_list, h.n_sched)};
+      copy_spans(hot, ghot, live);
+    }
     SSIM_TOC(t0, kPhLoadSave);
   }
+  // Requires the header stored (store_header) and in registers (the state after a step or a preemption).
   __device__ __forceinline__ void save_hot() {
     SSIM_TIC(t0);
-    if (hot != ghot) copy16(ghot, hot, O.hot_bytes);
+    if (hot != ghot) {
+      const int hi = live_hi();
+      const int lo = live_lo < hi ? live_lo : hi;
+      const Span spans[6] = {{0, O.stages >> 4}, {O.pools, 1 + JC}, stage_span(lo, hi), pool_span(lo, hi),
+                             list_span(O.active_stages, h.n_active_stages), list_span(O.sched_list, h.n_sched)};
+      copy_spans(ghot, hot, spans);
+    }
     SSIM_TOC(t0, kPhLoadSave);
   }
 
@@ -1134,14 +1224,30 @@ struct Sim {
     int16_t* aj = H<int16_t>(O.active_jobs);
     int16_t* as = H<int16_t>(O.active_stages);
     if (W::lane() == 0) aj[h.n_active_jobs] = (int16_t)j;
-    const int base = job_base(j), n = job_nst(j);
-    for (int k0 = 0; k0 <= n; k0 += W::kWidth) {  // pools of the job and its stages, active-stage list
+    const int base = job_base(j), n = job_nst(j), tsb = ldu(D.tpl_stage_base, (int)job_tpl(j));
+    for (int k0 = 0; k0 <= n; k0 += W::kWidth) {  // stage records, pools of the job and its stages, active list
       const int k = k0 + W::lane();
       if (k <= n) {
         const int p = (k == n) ? job_pool(j) : stage_pool(base + k);
         ps_init(pmeta(p), pool(p).tab);
         cfrom(p) = 0;
-        if (k < n) as[h.n_active_stages + k] = (int16_t)(base + k);
+        if (k < n) {
+          const int g = base + k, ts = tsb + k;
+          StageRec r;
+          r.job = (int16_t)j;
+          r.ts = (int16_t)ts;
+          r.rem = (int16_t)ldg(D.ts_num_tasks, ts);
+          r.exe = 0;
+          r.mov = 0;
+          r.com = 0;
+          r.unmet = (int8_t)(ldg(D.ts_parent_base, ts + 1) - ldg(D.ts_parent_base, ts));
+          r.sel = 0;
+          r.fw_keymask = (uint8_t)ldg(D.ts_fw_keymask, ts);
+          r.fw_maxlevel = (uint8_t)ldg(D.ts_fw_maxlevel, ts);
+          stage(g) = r;
+          recent()[g] = ldg(D.ts_rough, ts);
+          as[h.n_active_stages + k] = (int16_t)g;
+        }
       }
     }
     W::sync();
@@ -1281,7 +1387,10 @@ struct Sim {
   // The stop condition is a read of one shared word (TicketStop): polled every kStopEvery-th event, issued one
   // event before it is tested so its latency hides behind that event. Most steps take fewer events and finish
   // unpolled; the long ones (hundreds of task events) are the launch tail preemption removes.
-  static constexpr int kStopEvery = 8;
+#ifndef SSIM_STOP_EVERY
+#define SSIM_STOP_EVERY 8
+#endif
+  static constexpr int kStopEvery = SSIM_STOP_EVERY;  // a power of two
   template <class Stop>
   __device__ __forceinline__ int simulate(const Stop& stop) {  // _resume_simulation :320-343
     uint64_t tk = 0;
@@ -1810,27 +1919,8 @@ struct Sim {
       return;
     }
     W::sync();
-    // stages
-    for (int j = 0; j < nj; ++j) {
-      const int t = job_tpl(j), base = job_base(j), ns = job_nst(j), tsb = ldg(D.tpl_stage_base, t);
-      for (int k0 = 0; k0 < ns; k0 += W::kWidth) {
-        const int k = k0 + W::lane();
-        if (k < ns) {
-          const int g = base + k, ts = tsb + k;
-          st_job(g) = (int16_t)j;
-          st_ts(g) = (int16_t)ts;
-          st_rem(g) = (int16_t)ldg(D.ts_num_tasks, ts);
-          st_exe(g) = 0;
-          st_mov(g) = 0;
-          st_com(g) = 0;
-          st_unmet(g) = (int8_t)(ldg(D.ts_parent_base, ts + 1) - ldg(D.ts_parent_base, ts));
-          st_sel(g) = 0;
-          stage(g).fw_keymask = (uint8_t)ldg(D.ts_fw_keymask, ts);
-          stage(g).fw_maxlevel = (uint8_t)ldg(D.ts_fw_maxlevel, ts);
-          st_recent(g) = ldg(D.ts_rough, ts);
-        }
-      }
-    }
+    // stage records are initialised at arrival (on_job_arrival)
+    live_lo = 0;
     // executors, commitments, COMMON pool = set(range(N))
     for (int k0 = 0; k0 < NE; k0 += W::kWidth) {
       const int e = k0 + W::lane();

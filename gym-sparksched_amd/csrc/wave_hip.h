@@ -163,6 +163,14 @@ struct WaveHip {
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
   }
+  __device__ static __forceinline__ int min_i(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const int y = __shfl_xor(x, off);
+      x = y < x ? y : x;
+    }
+    return uni(x);
+  }
   __device__ static __forceinline__ int max_i(int x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

@@ -66,17 +66,21 @@ def main():
     native.LIB_PATH = os.path.join(REPO, "gym-sparksched_amd", "build", "libsparksched_prof.so")
     B = 1024
     eng = DeviceEngine(cfg, B, ds)
-    eng.reset(seeds=list(range(B)))
-    eng.rollout(_abi.SSIM_POLICY_RANDOM, 1, 20)
+    # the bench's batch: device reset, then a seeded pre-roll over the episodes' phases (bench.py step 2)
+    eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=list(range(B)))
+    pre = np.random.default_rng([0, 0, 7]).integers(0, 1000, B).astype(np.int32)
+    eng.rollout_steps(_abi.SSIM_POLICY_RANDOM, 4321, pre, 1001, flags=_abi.SSIM_ROLLOUT_AUTORESET)
     torch.cuda.synchronize()
-    d0 = eng.views["counts"][:, _abi.OC_DECISIONS].sum().item()
-    e0 = eng.views["counts"][:, _abi.OC_EVENTS].sum().item()
-    prof = torch.zeros((B, len(PHASES)), dtype=torch.int64, device=eng.device)
+    acc = eng.views["acc"]
+    d0 = acc[:, _abi.ACC_DECISIONS].sum().item()
+    e0 = acc[:, 3].sum().item()
+    # per env: the phase sums, then 4 s_memrealtime stamps (engine.h kTEntry..kTSaved)
+    prof = torch.zeros((B, len(PHASES) + 4), dtype=torch.int64, device=eng.device)
     lib.ssim_rollout_profiled(eng.handle, _abi.SSIM_POLICY_RANDOM, 1, K, prof.data_ptr(), eng._stream())
     torch.cuda.synchronize()
-    d1 = eng.views["counts"][:, _abi.OC_DECISIONS].sum().item()
-    e1 = eng.views["counts"][:, _abi.OC_EVENTS].sum().item()
-    p = prof.cpu().numpy().astype(np.float64)  # s_memtime ticks = shader cycles (MI355X_MICROARCH.md)
+    d1 = acc[:, _abi.ACC_DECISIONS].sum().item()
+    e1 = acc[:, 3].sum().item()
+    p = prof[:, :len(PHASES)].cpu().numpy().astype(np.float64)  # s_memtime ticks = shader cycles
     dec = d1 - d0
     tot = p.sum(axis=0)
     print(f"decisions {dec}, events {e1 - e0} ({(e1 - e0) / dec:.2f}/decision)")

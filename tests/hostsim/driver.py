@@ -59,6 +59,7 @@ def lib():
         L.hs_create.argtypes = [ct.POINTER(SsimConfig), ct.POINTER(SsimDataset), ct.POINTER(vp),
                                 ct.POINTER(SsimLayout)]
         L.hs_destroy.argtypes = [vp]
+        L.hs_set_resident.argtypes = [vp, ct.c_int]
         for n in ("hs_obs", "hs_reset_arena", "hs_state"):
             getattr(L, n).argtypes = [vp]
             getattr(L, n).restype = ct.POINTER(ct.c_uint8)
@@ -81,7 +82,7 @@ def lib():
 
 
 class HostEngine:
-    def __init__(self, env_cfg: dict, num_envs: int, dataset, job_cap=None, trace_cap: int = 0):
+    def __init__(self, env_cfg: dict, num_envs: int, dataset, job_cap=None, trace_cap: int = 0, resident=False):
         N = env_cfg["num_executors"]
         packed = dataset if isinstance(dataset, PackedDataset) else pack(dataset, N)
         self.packed = packed.with_executors(N)
@@ -95,6 +96,9 @@ class HostEngine:
         rc = lib().hs_create(ct.byref(self.cfg), ct.byref(self.ds), ct.byref(h), ct.byref(self.layout))
         assert rc == 0
         self.handle = h
+        # emulate the device's LDS residency (poisoned working copy of the hot block, the engine's own
+        # load_hot / save_hot around every step and rollout)
+        lib().hs_set_resident(h, 1 if resident else 0)
         L = self.layout
         self.obs = np.ctypeslib.as_array(lib().hs_obs(h), shape=(L.obs_bytes,))
         self.reset_buf = np.ctypeslib.as_array(lib().hs_reset_arena(h), shape=(L.reset_bytes,))

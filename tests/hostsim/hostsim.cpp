@@ -51,6 +51,7 @@ struct WaveSerial {
   static void amin(int* p, int v) { *p = v < *p ? v : *p; }
   static void aor(uint32_t* p, uint32_t v) { *p |= v; }
   static int max_i(int x) { return x; }
+  static int min_i(int x) { return x; }
   static void min_pair(int&, int&) {}
   template <int kSpan>
   static int argmin_event(double t, int, bool valid, double* tmin) {
@@ -65,7 +66,21 @@ struct hs_handle {
   uint8_t* obs;
   uint8_t* reset;
   uint8_t* scratch;
+  uint8_t* lds;   // emulated LDS residency: [hot copy | scratch] (hs_set_resident)
+  int resident;
 };
+
+// LDS-residency emulation (hs_set_resident): step and rollout calls run on a working copy of the hot block made by
+// the engine's own load_hot / save_hot, with the copy pre-filled with a poison byte, so a read of a record outside
+// the live range the copy covers (or a write the save drops) shows up as a parity failure on the CPU.
+static constexpr uint8_t kPoison = 0xA5;
+static uint8_t* resident_lds(hs_handle* h) {
+  const Params* P = h->params;
+  const int64_t n = P->O.hot_bytes + P->L.scratch_bytes;
+  if (h->lds == nullptr) h->lds = (uint8_t*)malloc((size_t)n);
+  memset(h->lds, kPoison, (size_t)n);
+  return h->lds;
+}
 
 extern "C" {
 
@@ -99,8 +114,11 @@ void hs_destroy(hs_handle* h) {
   free(h->obs);
   free(h->reset);
   free(h->scratch);
+  free(h->lds);
   free(h);
 }
+
+void hs_set_resident(hs_handle* h, int on) { h->resident = on; }
 
 uint8_t* hs_obs(hs_handle* h) { return h->obs; }
 uint8_t* hs_reset_arena(hs_handle* h) { return h->reset; }
@@ -118,11 +136,13 @@ int hs_reset(hs_handle* h) {
 int hs_step(hs_handle* h, const int32_t* stage_idx, const int32_t* num_exec) {
   const Params* P = h->params;
   for (int e = 0; e < P->L.num_envs; ++e) {
-    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
+    Sim<WaveSerial> s(P, h->state, h->resident ? resident_lds(h) : h->scratch, h->obs, e, h->resident != 0);
     StepIn a;
     a.stage_idx = stage_idx[e];
     a.num_exec = num_exec[e];
+    s.load_hot();  // (k_step's sequence; no-ops without residency)
     s.step(a);
+    s.save_hot();
   }
   return 0;
 }
@@ -169,9 +189,10 @@ int hs_rollout_steps(hs_handle* h, int kind, uint64_t seed, const int32_t* env_s
   const Params* P = h->params;
   const int B = P->L.num_envs;
   for (int e = 0; e < B; ++e) {
-    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
+    Sim<WaveSerial> s(P, h->state, h->resident ? resident_lds(h) : h->scratch, h->obs, e, h->resident != 0);
     PolicyView<WaveSerial> v{P->L, h->obs, e};
     const int steps = env_steps != nullptr && env_steps[e] < num_steps ? env_steps[e] : num_steps;
+    s.load_hot();
     for (int k = 0; k < steps; ++k) {
       // the device rollout's policy (picks from the hot block) must equal the obs-arena view's (k_policy)
       s.load_header();
@@ -188,6 +209,7 @@ int hs_rollout_steps(hs_handle* h, int kind, uint64_t seed, const int32_t* env_s
         s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits ? limits[e] : __builtin_inf(),
                         h->reset + (int64_t)e * P->L.reset_stride);
     }
+    s.save_hot();
   }
   return 0;
 }

@@ -7,12 +7,15 @@ import cases
 from spark_sched_sim import _abi
 
 
-@pytest.fixture(scope="module")
-def make():
+@pytest.fixture(scope="module", params=[False, True], ids=["hbm", "lds"])
+def make(request):
+    """`lds`: the device's LDS residency emulated (hostsim.cpp hs_set_resident): every step / rollout runs on a
+    working copy of the hot block made by the engine's own live-range load_hot / save_hot, pre-filled with poison,
+    so a record read outside the copied range or a write the save drops breaks parity here on the CPU."""
     from hostsim.driver import HostEngine
 
     def _make(cfg, B, ds, trace_cap):
-        return HostEngine(cfg, B, ds, trace_cap=trace_cap)
+        return HostEngine(cfg, B, ds, trace_cap=trace_cap, resident=request.param)
 
     return _make
 
