@@ -17,6 +17,7 @@
 // (`lds_resident`), and CPython-set tables are staged through LDS one pool at a time; HBM sees bulk
 // coalesced copies, the obs stores and the read-only dataset gathers.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include "layout.h"
@@ -96,6 +97,31 @@ struct NoStop {
 };
 enum : int32_t { kSimIdle = 0, kSimDecision = 1, kSimPreempted = 2 };
 
+// The launch constants the event loop reads (dataset pointers, config scalars, obs-arena offsets), filled on the
+// host by fill_hot_params. On device each lane of one VGPR holds one dword (Sim::hpv) and a field read is a
+// v_readlane with a constant lane: with the register pressure of the serial state machine the compiler otherwise
+// re-reads Params fields with scalar loads whose latency the loop then waits on, once per event.
+struct HotParams {
+  const int32_t* tpl_stage_base;
+  const int32_t* ts_num_tasks;
+  const double* ts_rough;
+  const int32_t* ts_child_base;
+  const int32_t* ts_children;
+  const int32_t* ts_parent_base;
+  const int32_t* ts_parents;
+  const int32_t* ts_fw_keymask;
+  const int32_t* ts_fw_maxlevel;
+  const int32_t* dur_off;
+  const int32_t* dur_len;
+  const double* durations;
+  const uint64_t* ts_topo;
+  double moving_delay, warmup_delay, beta, job_arrival_gap;
+  int64_t ob_nodes, ob_edge_links, ob_dag_ptr, ob_supplies, ob_frontier, ob_sched_rank, ob_counts, ob_reward,
+      ob_wall_time, ob_acc, ob_trace;
+  int32_t num_templates, trace_cap, edge_cap, job_arrival_cap, topo, pad;
+};
+static_assert(sizeof(HotParams) <= 256 && sizeof(HotParams) % 8 == 0, "one dword per lane of one VGPR");
+
 // Everything a launch needs besides the arenas. Lives at the start of the state arena (device memory),
 // so kernels take one pointer and read fields through the scalar cache.
 // Executor-key table per number of local executors n (tpch.py:216-235 on executor_intervals, tpch.py:237-262):
@@ -103,6 +129,7 @@ enum : int32_t { kSimIdle = 0, kSimDecision = 1, kSimPreempted = 2 };
 // the sampler's key choice is scalar-cache reads instead of two dependent dataset loads.
 constexpr int kIvRows = 256;
 struct Params {
+  HotParams hp;  // (first: 16-B aligned at the start of the state arena)
   ssim_layout L;
   StateOffsets O;
   ssim_dataset D;
@@ -140,6 +167,47 @@ inline bool fill_interval_table(Params* p, const double* intervals, int num_exec
   return true;
 }
 
+// Host side: Params::hp from the layout, dataset and config already in *p.
+inline void fill_hot_params(Params* p) {
+  HotParams& h = p->hp;
+  const ssim_dataset& D = p->D;
+  h.tpl_stage_base = D.tpl_stage_base;
+  h.ts_num_tasks = D.ts_num_tasks;
+  h.ts_rough = D.ts_rough;
+  h.ts_child_base = D.ts_child_base;
+  h.ts_children = D.ts_children;
+  h.ts_parent_base = D.ts_parent_base;
+  h.ts_parents = D.ts_parents;
+  h.ts_fw_keymask = D.ts_fw_keymask;
+  h.ts_fw_maxlevel = D.ts_fw_maxlevel;
+  h.dur_off = D.dur_off;
+  h.dur_len = D.dur_len;
+  h.durations = D.durations;
+  h.ts_topo = D.ts_topo;
+  h.moving_delay = p->C.moving_delay;
+  h.warmup_delay = p->C.warmup_delay;
+  h.beta = p->C.beta;
+  h.job_arrival_gap = p->C.job_arrival_gap;
+  const ssim_layout& L = p->L;
+  h.ob_nodes = L.ob_nodes;
+  h.ob_edge_links = L.ob_edge_links;
+  h.ob_dag_ptr = L.ob_dag_ptr;
+  h.ob_supplies = L.ob_supplies;
+  h.ob_frontier = L.ob_frontier;
+  h.ob_sched_rank = L.ob_sched_rank;
+  h.ob_counts = L.ob_counts;
+  h.ob_reward = L.ob_reward;
+  h.ob_wall_time = L.ob_wall_time;
+  h.ob_acc = L.ob_acc;
+  h.ob_trace = L.ob_trace;
+  h.num_templates = D.num_templates;
+  h.trace_cap = L.trace_cap;
+  h.edge_cap = L.edge_cap;
+  h.job_arrival_cap = p->C.job_arrival_cap;
+  h.topo = (p->C.max_stages <= 32 && D.ts_topo != nullptr) ? 1 : 0;
+  h.pad = 0;
+}
+
 // kN / kJ / kS: executor count, job cap and stage cap as compile-time constants (0 = read from the layout at
 // run time). A fully specialised instantiation sees every section offset (hot block, scratch), loop bound
 // and table size as a constant, so LDS accesses use immediate offsets and no SGPRs hold offsets.
@@ -160,6 +228,8 @@ struct Sim {
   EnvHeader h;    // register copy of the header
   Pcg64 rng;
   uint32_t iv_lane;  // Params::iv row `lane` (device: read with v_readlane instead of a scalar-cache load)
+  const HotParams* HPp;  // host build: Params::hp read in place
+  uint32_t hpv;          // device: dword `lane` of Params::hp
 #ifdef SSIM_PROFILE
   uint64_t prof[kNumPhases] = {0};
 #endif
@@ -174,7 +244,27 @@ struct Sim {
         cold(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes + O.hot_bytes),
         scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index) {
     iv_lane = W::lane() < kIvRows ? *reinterpret_cast<const uint32_t*>(IV[W::lane()]) : 0u;
+    HPp = &p->hp;
+    hpv = (W::kWidth == 64 && W::lane() < (int)(sizeof(HotParams) / 4)) ? reinterpret_cast<const uint32_t*>(&p->hp)[W::lane()]
+                                                                      : 0u;
   }
+  // A HotParams field: v_readlane of hpv on device (constant lanes), the field itself in the host build.
+  template <class T, int kOff>
+  __device__ __forceinline__ T hp_get(const T& host_val) const {
+    if constexpr (W::kWidth == 64) {
+      static_assert(kOff % 4 == 0, "dword fields");
+      if constexpr (sizeof(T) == 8) {
+        const uint32_t lo = (uint32_t)W::bcast_i((int)hpv, kOff / 4);
+        const uint32_t hi = (uint32_t)W::bcast_i((int)hpv, kOff / 4 + 1);
+        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+      } else {
+        return __builtin_bit_cast(T, (uint32_t)W::bcast_i((int)hpv, kOff / 4));
+      }
+    } else {
+      return host_val;
+    }
+  }
+#define HP(f) hp_get<decltype(HotParams::f), (int)offsetof(HotParams, f)>(HPp->f)
 
   // ---------------------------------------------------------------- hot-block residency
   // LDS residency copies only the LIVE part of the hot block: the fixed sections (header, jobs, executors,
@@ -890,9 +980,9 @@ struct Sim {
   }
 
   __device__ __forceinline__ void trace(double t, int kind, int e, int job, int sid, int seq) {
-    if (L.trace_cap == 0) return;  // tracing off: no bookkeeping at all
-    if (h.trace_len < L.trace_cap && W::lane() == 0) {
-      TraceRec* r = reinterpret_cast<TraceRec*>(obs + L.ob_trace) + (int64_t)eid * L.trace_cap + h.trace_len;
+    if (HP(trace_cap) == 0) return;  // tracing off: no bookkeeping at all
+    if (h.trace_len < HP(trace_cap) && W::lane() == 0) {
+      TraceRec* r = reinterpret_cast<TraceRec*>(obs + HP(ob_trace)) + (int64_t)eid * HP(trace_cap) + h.trace_len;
       r->t = t;
       r->kind = kind;
       r->exec = e;
@@ -917,8 +1007,8 @@ struct Sim {
       const int l = W::lane();
       if (l < 24) {
         const int idx = (ts * 3 + (l >> 3)) * kNumLevels + (l & 7);
-        d.len = ldg(D.dur_len, idx);
-        d.off = ldg(D.dur_off, idx);
+        d.len = ldg(HP(dur_len), idx);
+        d.off = ldg(HP(dur_off), idx);
       }
     }
     return d;
@@ -930,13 +1020,13 @@ struct Sim {
       off = W::bcast_i(dd.off, wave * 8 + level);
     } else {
       const int idx = (ts * 3 + wave) * kNumLevels + level;
-      len = ldu(D.dur_len, idx);
-      off = ldu(D.dur_off, idx);
+      len = ldu(HP(dur_len), idx);
+      off = ldu(HP(dur_off), idx);
     }
     if (len <= 0) return false;  // KeyError (missing) or ValueError (empty): no RNG consumed
     SSIM_TIC(t0);
     const uint32_t k = rng.bounded((uint32_t)len);
-    *out = ldu(D.durations, off + (int)k);
+    *out = ldu(HP(durations), off + (int)k);
     SSIM_TOC(t0, kPhDraw);
     return true;
   }
@@ -967,7 +1057,7 @@ struct Sim {
     double d = 0.0;
     if (last < 0) {
       if (draw(ts, dd, 0, level, &d)) return d;
-      if (draw(ts, dd, 1, level, &d)) return d + C.warmup_delay;
+      if (draw(ts, dd, 1, level, &d)) return d + HP(warmup_delay);
       fail(SSIM_ERR_SAMPLER);
       return 0.0;
     }
@@ -992,7 +1082,7 @@ struct Sim {
     if (s.rem - (s.mov + s.com) <= 0) return false;
     const int base = jr.base;
     if (topo_masks()) {  // one dataset load for all parents, then their records
-      uint32_t pm = (uint32_t)ldg(D.ts_topo, s.ts);
+      uint32_t pm = (uint32_t)ldg(HP(ts_topo), s.ts);
       while (pm) {
         const StageRec ps = stage(base + __builtin_ctz(pm));
         pm &= pm - 1;
@@ -1000,15 +1090,15 @@ struct Sim {
       }
       return true;
     }
-    for (int k = ldg(D.ts_parent_base, s.ts); k < ldg(D.ts_parent_base, s.ts + 1); ++k) {
-      const StageRec ps = stage(base + ldg(D.ts_parents, k));
+    for (int k = ldg(HP(ts_parent_base), s.ts); k < ldg(HP(ts_parent_base), s.ts + 1); ++k) {
+      const StageRec ps = stage(base + ldg(HP(ts_parents), k));
       if (ps.rem - (ps.mov + ps.com) > 0) return false;
     }
     return true;
   }
 
   // Templates of <= 32 stages: the DAG neighbourhood of a stage as bit sets (ssim_dataset.ts_topo)
-  __device__ __forceinline__ bool topo_masks() const { return C.max_stages <= 32 && D.ts_topo != nullptr; }
+  __device__ __forceinline__ bool topo_masks() const { return HP(topo) != 0; }
 
   // first schedulable stage in node order, or -1
   __device__ __forceinline__ int scan_first(int mode, int jx, int src_job) {
@@ -1110,7 +1200,7 @@ struct Sim {
     check(ex_job(e) != st_job(g));
     move_to_pool(e, stage_pool(g), true);
     if (ex_job(e) >= 0) detach(ex_job(e), e);
-    push_event(e, h.wall + C.moving_delay, kEvReady, g);
+    push_event(e, h.wall + HP(moving_delay), kEvReady, g);
   }
 
   // _move_idle_executors (:745-782) with an explicit executor list (n ids in `ids`).
@@ -1128,7 +1218,7 @@ struct Sim {
       move_to_pool(e, dst, false);
       if (dst == kPoolCommon) {
         detach(j, e);
-        if (L.trace_cap > 0) trace(h.wall, kTrToCommon, e, j, -1, -1);
+        if (HP(trace_cap) > 0) trace(h.wall, kTrToCommon, e, j, -1, -1);
       }
     }
   }
@@ -1224,7 +1314,7 @@ struct Sim {
     int16_t* aj = H<int16_t>(O.active_jobs);
     int16_t* as = H<int16_t>(O.active_stages);
     if (W::lane() == 0) aj[h.n_active_jobs] = (int16_t)j;
-    const int base = job_base(j), n = job_nst(j), tsb = ldu(D.tpl_stage_base, (int)job_tpl(j));
+    const int base = job_base(j), n = job_nst(j), tsb = ldu(HP(tpl_stage_base), (int)job_tpl(j));
     for (int k0 = 0; k0 <= n; k0 += W::kWidth) {  // stage records, pools of the job and its stages, active list
       const int k = k0 + W::lane();
       if (k <= n) {
@@ -1236,16 +1326,16 @@ struct Sim {
           StageRec r;
           r.job = (int16_t)j;
           r.ts = (int16_t)ts;
-          r.rem = (int16_t)ldg(D.ts_num_tasks, ts);
+          r.rem = (int16_t)ldg(HP(ts_num_tasks), ts);
           r.exe = 0;
           r.mov = 0;
           r.com = 0;
-          r.unmet = (int8_t)(ldg(D.ts_parent_base, ts + 1) - ldg(D.ts_parent_base, ts));
+          r.unmet = (int8_t)(ldg(HP(ts_parent_base), ts + 1) - ldg(HP(ts_parent_base), ts));
           r.sel = 0;
-          r.fw_keymask = (uint8_t)ldg(D.ts_fw_keymask, ts);
-          r.fw_maxlevel = (uint8_t)ldg(D.ts_fw_maxlevel, ts);
+          r.fw_keymask = (uint8_t)ldg(HP(ts_fw_keymask), ts);
+          r.fw_maxlevel = (uint8_t)ldg(HP(ts_fw_maxlevel), ts);
           stage(g) = r;
-          recent()[g] = ldg(D.ts_rough, ts);
+          recent()[g] = ldg(HP(ts_rough), ts);
           as[h.n_active_stages + k] = (int16_t)g;
         }
       }
@@ -1275,7 +1365,7 @@ struct Sim {
     const int ts = st_ts(g), base = job_base(j);
     bool changed = false;
     if (topo_masks()) {
-      uint32_t cm = (uint32_t)(ldu(D.ts_topo, ts) >> 32);
+      uint32_t cm = (uint32_t)(ldu(HP(ts_topo), ts) >> 32);
       while (cm) {
         const int c = base + __builtin_ctz(cm);
         cm &= cm - 1;
@@ -1284,9 +1374,9 @@ struct Sim {
       }
       return changed;
     }
-    const int kb = ldu(D.ts_child_base, ts), ke = ldu(D.ts_child_base, ts + 1);
+    const int kb = ldu(HP(ts_child_base), ts), ke = ldu(HP(ts_child_base), ts + 1);
     for (int k = kb; k < ke; ++k) {
-      const int c = base + ldu(D.ts_children, k);
+      const int c = base + ldu(HP(ts_children), k);
       st_unmet(c) -= 1;
       if (st_unmet(c) == 0 && !st_completed(c)) changed = true;
     }
@@ -1317,6 +1407,7 @@ struct Sim {
       run_next_task_rec(g, s, x, dd);
       stage(g) = s;
       exr(e) = x;
+      SSIM_MARK("task_done_fast_end");
       return;
     }
     stage(g) = s;
@@ -1399,10 +1490,8 @@ struct Sim {
       if (frozen()) return kSimIdle;
       if (Stop::kCan) {
         const int ph = n++ & (kStopEvery - 1);
-        if (ph == kStopEvery - 1)
-          tk = stop.issue();
-        else if (ph == 0 && n > 1 && stop.hit(tk))
-          return kSimPreempted;
+        if (ph == 0 && n > 1 && stop.hit(tk)) return kSimPreempted;  // the value issued one event ago
+        if (ph == kStopEvery - 1) tk = stop.issue();
       }
       double t;
       int kind, e, g, seq;
@@ -1417,12 +1506,12 @@ struct Sim {
       h.events++;
       h.step_events++;
       if (kind == kEvArrival) {
-        if (L.trace_cap > 0) trace(t, kind, -1, g, -1, seq);
+        if (HP(trace_cap) > 0) trace(t, kind, -1, g, -1, seq);
         SSIM_TIC(t_a);
         on_job_arrival(g);
         SSIM_TOC(t_a, kPhJobArr);
       } else {
-        if (L.trace_cap > 0) {
+        if (HP(trace_cap) > 0) {
           const int j = st_job(g);
           trace(t, kind, e, j, g - job_base(j), seq);
         }
@@ -1470,28 +1559,40 @@ struct Sim {
           const double a = ta > t0 ? ta : t0;
           const double tc = st == kJobDone ? jt.tdone : h.wall;
           const double b = tc < h.wall ? tc : h.wall;
-          if (C.beta == 0.0)
+          if (HP(beta) == 0.0)
             part += b - a;
           else
-            part += exp(-C.beta * 1e-3 * (a - t0)) - exp(-C.beta * 1e-3 * (b - t0));
+            part += exp(-HP(beta) * 1e-3 * (a - t0)) - exp(-HP(beta) * 1e-3 * (b - t0));
         }
       }
     }
     double total = W::sum_d(part);
-    if (C.beta > 0.0) total /= C.beta;
+    if (HP(beta) > 0.0) total /= HP(beta);
     return total;
   }
 
   // ---------------------------------------------------------------- observation (:345-406, utils.py)
+  // Observation-arena stores: written once per decision and never read back by the kernel, so (SSIM_NT_OBS) they
+  // are non-temporal and do not evict the dataset's duration pools from L2.
+#ifndef SSIM_NT_OBS
+#define SSIM_NT_OBS 1
+#endif
+  template <class T>
+  __device__ __forceinline__ static void obs_st(T* p, T v) {
+    if constexpr (SSIM_NT_OBS && W::kWidth == 64)
+      W::st_nt(p, v);
+    else
+      *p = v;
+  }
   __device__ __forceinline__ void observe(double reward) {
     const int n = h.n_active_stages;
     const int src_job = source_job();
     const int16_t* act = H<int16_t>(O.active_stages);
     int16_t* sched = H<int16_t>(O.sched_list);
     int16_t* row_of = S<int16_t>(O.sc_row_of);
-    float* nodes = reinterpret_cast<float*>(obs + L.ob_nodes) + (int64_t)eid * SC * 3;
-    uint8_t* front = obs + L.ob_frontier + (int64_t)eid * SC;
-    int32_t* srank = reinterpret_cast<int32_t*>(obs + L.ob_sched_rank) + (int64_t)eid * SC;
+    float* nodes = reinterpret_cast<float*>(obs + HP(ob_nodes)) + (int64_t)eid * SC * 3;
+    uint8_t* front = obs + HP(ob_frontier) + (int64_t)eid * SC;
+    int32_t* srank = reinterpret_cast<int32_t*>(obs + HP(ob_sched_rank)) + (int64_t)eid * SC;
     // picks[j] (job id j): heuristics/utils.py find_stage of the job, packed as a min key over its
     // schedulable nodes: (frontier ? 0 : 1 << 16) | schedulable rank; INT32_MAX = none. Nodes of a job are
     // contiguous in node order and ranks grow with node order, so the min is the first frontier stage,
@@ -1513,11 +1614,11 @@ struct Sim {
       const int r = nsched + W::rank(m);
       if (ok) {
         const StageRec sr = stage(g);
-        nodes[3 * i + 0] = (float)sr.rem;
-        nodes[3 * i + 1] = (float)recent()[g];
-        nodes[3 * i + 2] = s ? 1.0f : 0.0f;
-        front[i] = sr.unmet == 0 ? 1 : 0;
-        srank[i] = s ? r : -1;
+        obs_st(nodes + 3 * i + 0, (float)sr.rem);
+        obs_st(nodes + 3 * i + 1, (float)recent()[g]);
+        obs_st(nodes + 3 * i + 2, s ? 1.0f : 0.0f);
+        obs_st(front + i, (uint8_t)(sr.unmet == 0 ? 1 : 0));
+        obs_st(srank + i, s ? r : -1);
         row_of[g] = (int16_t)i;
         if (s) {
           sched[r] = (int16_t)g;
@@ -1530,8 +1631,8 @@ struct Sim {
     // jobs: dag_ptr, exec_supplies, source_job_idx
     const int nj = h.n_active_jobs;
     const int16_t* aj = H<int16_t>(O.active_jobs);
-    int32_t* ptr = reinterpret_cast<int32_t*>(obs + L.ob_dag_ptr) + (int64_t)eid * (JC + 1);
-    int32_t* sup = reinterpret_cast<int32_t*>(obs + L.ob_supplies) + (int64_t)eid * JC;
+    int32_t* ptr = reinterpret_cast<int32_t*>(obs + HP(ob_dag_ptr)) + (int64_t)eid * (JC + 1);
+    int32_t* sup = reinterpret_cast<int32_t*>(obs + HP(ob_supplies)) + (int64_t)eid * JC;
     int src_idx = nj, run = 0;
     for (int k0 = 0; k0 < nj; k0 += W::kWidth) {
       const int k = k0 + W::lane();
@@ -1542,17 +1643,17 @@ struct Sim {
       int total = 0;
       const int ex = W::excl_scan(cnt, &total);
       if (ok) {
-        ptr[k] = run + ex;
-        sup[k] = jr.supply;
+        obs_st(ptr + k, run + ex);
+        obs_st(sup + k, (int32_t)jr.supply);
       }
       const uint64_t ms = W::ballot(ok && j == src_job);
       if (ms) src_idx = k0 + W::ffs(ms);
       run += total;
     }
-    if (W::lane() == 0) ptr[nj] = run;
+    if (W::lane() == 0) obs_st(ptr + nj, run);
     check(run == n);
     // edges: (row(u), row(v)) for active u, child v active; order = node order, children ascending
-    int64_t* links = reinterpret_cast<int64_t*>(obs + L.ob_edge_links) + (int64_t)eid * L.edge_cap * 2;
+    int64_t* links = reinterpret_cast<int64_t*>(obs + HP(ob_edge_links)) + (int64_t)eid * HP(edge_cap) * 2;
     int ne = 0;
     for (int i0 = 0; i0 < n; i0 += W::kWidth) {
       const int i = i0 + W::lane();
@@ -1564,7 +1665,7 @@ struct Sim {
         const StageRec sr = stage(g);
         base = job(sr.job).base;
         if (topo_masks()) {
-          uint32_t cm = (uint32_t)(ldg(D.ts_topo, sr.ts) >> 32);
+          uint32_t cm = (uint32_t)(ldg(HP(ts_topo), sr.ts) >> 32);
           while (cm) {
             const int b = __builtin_ctz(cm);
             cm &= cm - 1;
@@ -1573,10 +1674,10 @@ struct Sim {
           }
           cnt = __builtin_popcount(live);
         } else {
-          cb = ldg(D.ts_child_base, sr.ts);
-          ce = ldg(D.ts_child_base, sr.ts + 1);
+          cb = ldg(HP(ts_child_base), sr.ts);
+          ce = ldg(HP(ts_child_base), sr.ts + 1);
           for (int k = cb; k < ce; ++k) {
-            const StageRec c = stage(base + ldg(D.ts_children, k));
+            const StageRec c = stage(base + ldg(HP(ts_children), k));
             if (!(c.rem == 0 && c.exe == 0)) cnt++;
           }
         }
@@ -1586,20 +1687,20 @@ struct Sim {
       if (ok) {
         int o = ne + ex;
         if (topo_masks()) {
-          while (live && o < L.edge_cap) {
+          while (live && o < HP(edge_cap)) {
             const int c = base + __builtin_ctz(live);
             live &= live - 1;
-            links[2 * o + 0] = i;
-            links[2 * o + 1] = row_of[c];
+            obs_st(links + 2 * o + 0, (int64_t)i);
+            obs_st(links + 2 * o + 1, (int64_t)row_of[c]);
             o++;
           }
         } else {
           for (int k = cb; k < ce; ++k) {
-            const int c = base + ldg(D.ts_children, k);
+            const int c = base + ldg(HP(ts_children), k);
             const StageRec cr = stage(c);
-            if (!(cr.rem == 0 && cr.exe == 0) && o < L.edge_cap) {
-              links[2 * o + 0] = i;
-              links[2 * o + 1] = row_of[c];
+            if (!(cr.rem == 0 && cr.exe == 0) && o < HP(edge_cap)) {
+              obs_st(links + 2 * o + 0, (int64_t)i);
+              obs_st(links + 2 * o + 1, (int64_t)row_of[c]);
               o++;
             }
           }
@@ -1607,7 +1708,7 @@ struct Sim {
       }
       ne += total;
     }
-    if (ne > L.edge_cap) fail(SSIM_ERR_CAPACITY);
+    if (ne > HP(edge_cap)) fail(SSIM_ERR_CAPACITY);
     h.n_sched = nsched;
     h.src_idx = src_idx;
     h.stage_idx_n = n + 1;
@@ -1619,7 +1720,7 @@ struct Sim {
     *H<EnvAcc>(O.acc) = a;
     W::sync();
     if (W::lane() == 0) {
-      int64_t* acc = reinterpret_cast<int64_t*>(obs + L.ob_acc) + (int64_t)eid * kNumAcc;
+      int64_t* acc = reinterpret_cast<int64_t*>(obs + HP(ob_acc)) + (int64_t)eid * kNumAcc;
       acc[0] = a.nodes;
       acc[1] = a.edges;
       acc[2] = a.jobs;
@@ -1628,7 +1729,7 @@ struct Sim {
       acc[5] = a.episodes;
       acc[6] = 0;
       acc[7] = 0;
-      int32_t* cnts = reinterpret_cast<int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
+      int32_t* cnts = reinterpret_cast<int32_t*>(obs + HP(ob_counts)) + (int64_t)eid * SSIM_NUM_COUNTS;
       cnts[SSIM_OC_NUM_NODES] = n;
       cnts[SSIM_OC_NUM_EDGES] = ne;
       cnts[SSIM_OC_NUM_JOBS] = nj;
@@ -1645,8 +1746,8 @@ struct Sim {
       cnts[SSIM_OC_TRACE_LEN] = h.trace_len;
       cnts[SSIM_OC_STEP_EVENTS] = h.step_events;
       cnts[SSIM_OC_EPISODE] = h.episode;
-      reinterpret_cast<double*>(obs + L.ob_reward)[eid] = reward;
-      reinterpret_cast<double*>(obs + L.ob_wall_time)[eid] = h.wall;
+      reinterpret_cast<double*>(obs + HP(ob_reward))[eid] = reward;
+      reinterpret_cast<double*>(obs + HP(ob_wall_time))[eid] = h.wall;
     }
     W::sync();
   }
@@ -1654,7 +1755,7 @@ struct Sim {
   __device__ __forceinline__ void write_err_only(uint32_t transient) {
     W::sync();
     if (W::lane() == 0) {
-      int32_t* cnts = reinterpret_cast<int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
+      int32_t* cnts = reinterpret_cast<int32_t*>(obs + HP(ob_counts)) + (int64_t)eid * SSIM_NUM_COUNTS;
       cnts[SSIM_OC_ERR] = (int32_t)(h.err | transient);
     }
     W::sync();
@@ -1799,7 +1900,7 @@ struct Sim {
   __device__ __forceinline__ int sample_job_sequence(double time_limit, uint8_t* rec_base) {
     double* tarr = reinterpret_cast<double*>(rec_base + kResetHeadBytes);
     int32_t* tpl = reinterpret_cast<int32_t*>(rec_base + kResetHeadBytes + 8 * (int64_t)JC);
-    const int cap = C.job_arrival_cap;
+    const int cap = HP(job_arrival_cap);
     double t = 0.0;
     int k = 0;
     while (t < time_limit && (cap == 0 || k < cap)) {
@@ -1810,7 +1911,7 @@ struct Sim {
         tpl[k] = (q - 1) * 7 + sz;
         tarr[k] = t;
       }
-      t += C.job_arrival_gap * rng.std_exponential();
+      t += HP(job_arrival_gap) * rng.std_exponential();
       k++;
     }
     return k;
@@ -1828,7 +1929,7 @@ struct Sim {
       return;
     }
     int n = 0;
-    if (!(time_limit == __builtin_inf() && C.job_arrival_cap == 0) && C.job_arrival_gap > 0.0)
+    if (!(time_limit == __builtin_inf() && HP(job_arrival_cap) == 0) && HP(job_arrival_gap) > 0.0)
       n = sample_job_sequence(time_limit, rec_base);
     ssim_reset_record* rec = reinterpret_cast<ssim_reset_record*>(rec_base);
     if (W::lane() == 0) {
@@ -1890,8 +1991,8 @@ struct Sim {
       const int j = j0 + W::lane();
       const bool ok = j < nj;
       const int t = ok ? tpl[j] : 0;
-      const bool tb = ok && (t < 0 || t >= D.num_templates);
-      const int ns = (ok && !tb) ? ldg(D.tpl_stage_base, t + 1) - ldg(D.tpl_stage_base, t) : 0;
+      const bool tb = ok && (t < 0 || t >= HP(num_templates));
+      const int ns = (ok && !tb) ? ldg(HP(tpl_stage_base), t + 1) - ldg(HP(tpl_stage_base), t) : 0;
       int total = 0;
       const int ex = W::excl_scan(ns, &total);
       if (ok) {

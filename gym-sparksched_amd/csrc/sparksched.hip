@@ -164,6 +164,7 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
   }
   h->params.D = *dataset;
   h->params.C = *cfg;
+  fill_hot_params(&h->params);
   h->state = static_cast<uint8_t*>(state_arena);
   h->obs = static_cast<uint8_t*>(obs_arena);
   h->reset = static_cast<uint8_t*>(reset_arena);

@@ -145,6 +145,9 @@ struct WaveHip {
   // correctly rounded f32 ops (the reference's numpy float32 arithmetic; no contraction)
   __device__ static __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
   __device__ static __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+  // streaming (non-temporal) global store
+  template <class T>
+  __device__ static __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
   // LDS atomics / loads for lane-parallel relaxations
   __device__ static __forceinline__ int lds_load(const int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
   __device__ static __forceinline__ void amax(int* p, int v) { atomicMax(p, v); }

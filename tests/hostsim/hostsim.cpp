@@ -94,6 +94,7 @@ int hs_create(const ssim_config* cfg, const ssim_dataset* ds, hs_handle** out, s
   }
   p.D = *ds;
   p.C = *cfg;
+  fill_hot_params(&p);
   if (!fill_interval_table(&p, ds->intervals, cfg->num_executors)) {
     free(h);
     return -2;
