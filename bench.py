@@ -441,21 +441,22 @@ def main():
             pre = 0 if args.no_preempt else _abi.SSIM_ROLLOUT_PREEMPT
             eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=f | pre, time_limits=limits)
 
+    def launch_sizes(n, chunk=None):
+        chunk = chunk or n
+        return [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
+
     def run(n, events=None, chunk=None):
-        """n steps; `events` (list of HIP event pairs) brackets each kernel launch on the launch stream."""
+        """n steps; `events` (pre-created HIP event pairs, one per kernel launch) bracket each launch on the launch
+        stream."""
         if n <= 0:
             return
         if mode == "rollout":
-            chunk = chunk or n
-            sizes = [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
-            for c in sizes:
+            for i, c in enumerate(launch_sizes(n, chunk)):
                 if events is not None:
-                    e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                    e[0].record(stream)
+                    events[i][0].record(stream)
                 rollout_launch(c, events is not None)
                 if events is not None:
-                    e[1].record(stream)
-                    events.append(e)
+                    events[i][1].record(stream)
             return
         for k in range(n):
             if mode == "decima":
@@ -471,12 +472,10 @@ def main():
                 si, ne = eng.policy(kind, 1234, run.counter)
                 run.counter += 1
             if events is not None:
-                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                e[0].record(stream)
+                events[k][0].record(stream)
             eng.step(si, ne)
             if events is not None:
-                e[1].record(stream)
-                events.append(e)
+                events[k][1].record(stream)
             if mode == "decima":
                 done = ((cnt[:, _abi.OC_TERMINATED] != 0) | (cnt[:, _abi.OC_TRUNCATED] != 0)).to(torch.uint8)
                 eng.reset_sampled(done, time_limits=limits)  # finished episodes: reset(seed=None) on device
@@ -486,7 +485,11 @@ def main():
     run(W)
     sync()
     acc0 = np.array(eng.to_numpy(eng.views["acc"]), dtype=np.int64).copy()
-    events = None if host else []
+    events = None
+    if not host:  # created before the timed region (event creation is host work, not part of a step)
+        n_launch = len(launch_sizes(K, args.chunk or K)) if mode == "rollout" else K
+        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(n_launch)]
     if world > 1:
         dist.barrier()
     sync()

@@ -69,8 +69,9 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
                  kCtPoolSmall, kCtPoolBig, kCtTask, kCtIdleOrder,
                  // histogram of whole-decision cycles (policy + step + auto-reset): bucket b = [2^(b+10), 2^(b+11))
                  kHist0,
-                 // s_memrealtime stamps (100 MHz chip clock): wave entry, hot block loaded, loop exit, hot block saved
-                 kTEntry = kHist0 + 16, kTLoaded, kTLoopEnd, kTSaved, kNumPhases };
+                 // s_memrealtime stamps (100 MHz chip clock): wave entry, hot block loaded, loop exit, hot block saved, engine
+                 // constructed, fixed sections copied
+                 kTEntry = kHist0 + 16, kTLoaded, kTLoopEnd, kTSaved, kTCtor, kTCopy1, kNumPhases };
 #ifdef SSIM_PROFILE
 #define SSIM_COUNT(ph) prof[ph] += 1
 #else
@@ -319,6 +320,9 @@ struct Sim {
     if (hot != ghot) {
       const Span fixed[2] = {{0, O.stages >> 4}, {O.pools, 1 + JC}};
       copy_spans(hot, ghot, fixed);
+#ifdef SSIM_PROFILE
+      prof[kTCopy1] = __builtin_amdgcn_s_memrealtime();
+#endif
       load_header();
       // lowest stage still referenced (jobs' stages are contiguous in arrival order): the stages of the active
       // jobs, and stage pools / stages a completed job can still be named by — an executor left in one of its

@@ -107,11 +107,14 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
     if (num_steps <= 0) return;
   }
   const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
-  if (env_idle(P, state, eid) && action_log == nullptr && !autoreset) return;
+  if (!autoreset && action_log == nullptr && env_idle(P, state, eid)) return;
 #ifdef SSIM_PROFILE
   const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime();
 #endif
   Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
+#ifdef SSIM_PROFILE
+  s.prof[kTCtor] = __builtin_amdgcn_s_memrealtime();
+#endif
   s.load_hot();
 #ifdef SSIM_PROFILE
   s.prof[kTEntry] = rt_entry;
@@ -136,6 +139,17 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
     const uint64_t t0 = WaveHip::clock();
 #endif
     s.load_header();
+    // episode over (terminated, or truncated by the time limit): reset(seed=None) in place, before anything else
+    // (one call site for the whole loop). A preemptible budget launch resets only when it holds a claimed
+    // decision for the new episode: an episode that ends as the budget runs out is reset at the start of the
+    // env's next launch, so no wave spends the end of a launch on a reset.
+    if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit) &&
+        !s.pending()) {  // (a step preempted past the time limit completes first)
+      if (stop.on && granted == 0 && (granted = stop.claim(B, last)) == 0) break;
+      s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
+                      reset + (int64_t)eid * P->L.reset_stride);
+      continue;
+    }
     double st0 = 0.0;
     bool simulate;
     if (s.pending()) {  // completes first, whatever this launch's mode; not one of its num_steps
@@ -161,10 +175,6 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
       simulate = s.step_begin(a, &st0);
     }
     if (simulate && !s.finish_step(st0, stop)) break;  // preempted mid-simulation: pending until the next launch
-    // episode over (terminated, or truncated by the time limit): reset(seed=None) in place
-    if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit))
-      s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
-                      reset + (int64_t)eid * P->L.reset_stride);
 #ifdef SSIM_PROFILE
     {
       const uint64_t dc = WaveHip::clock() - t0;

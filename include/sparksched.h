@@ -194,7 +194,9 @@ int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
 /* ssim_rollout_budget only: once the budget is spent, an env in the middle of a step stops at the next event
  * boundary instead of finishing the step (the launch ends within ~one event rather than ~the longest step);
  * the step stays pending (SSIM_ERR_PENDING) and the next launch on the handle completes it first. Decisions
- * are counted when they complete (ob_acc), so back-to-back launches count every decision exactly once. */
+ * are counted when they complete (ob_acc), so back-to-back launches count every decision exactly once. With
+ * SSIM_ROLLOUT_AUTORESET an episode that ends once the budget is spent is reset at the start of the env's next
+ * launch (before its next decision), so until then its observation is the terminal one. */
 #define SSIM_ROLLOUT_PREEMPT 0x2
 /* Same rollout, launched under the kernel symbol k_rollout_warmup instead of k_rollout, so a profiler's per-kernel
  * statistics can tell launches that are not measured (a benchmark's pre-roll and warm-up) from measured ones. */

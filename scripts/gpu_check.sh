@@ -34,6 +34,7 @@ for s in "$@"; do
     ab)      step ab 900 bash scripts/ab_tpch.sh ;;
     cpubase) step cpubase 900 python scripts/cpu_baselines.py ;;
     abargs)  step abargs 900 bash scripts/ab_args.sh ;;
+    overhead) step overhead 300 python scripts/launch_overhead.py ;;
     launch)  step launch 600 python scripts/launch_profile.py ;;
     prof_driver) step prof_driver 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_driver" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 ;;
     ab20np)  step ab20np 900 env AB_TAG=s20np AB_ARGS="--steps 20 --warmup 5 --no-preempt" bash scripts/ab_tpch.sh ;;

@@ -32,7 +32,7 @@ def main():
     cfg = {"num_executors": 10, "job_arrival_cap": 50, "job_arrival_rate": 4.0e-5, "moving_delay": 2000.0,
            "warmup_delay": 1000.0}
     B = 1024
-    nph = len(PP.PHASES) + 4
+    nph = len(PP.PHASES) + PP.NSTAMPS
     res = {}
     for K in (20, 300):
         for preempt in (False, True):
@@ -57,13 +57,16 @@ def main():
                 if rep == 0:
                     continue
                 p = prof.cpu().numpy()
-                st = p[:, -4:].astype(np.float64) * 10.0  # ns (100 MHz)
-                entry, loaded, loopend, saved = st.T
+                st = p[:, -PP.NSTAMPS:].astype(np.float64) * 10.0  # ns (100 MHz)
+                entry, loaded, loopend, saved, ctor, copy1 = st.T
                 t0 = entry.min()
                 le = np.sort(loopend - t0)
                 out.append({"event_ms": ev[0].elapsed_time(ev[1]), "decisions": a1 - a0,
                             "entry_skew_us": (entry.max() - t0) / 1e3,
                             "load_us_p50": float(np.median(loaded - entry)) / 1e3,
+                            "ctor_us_p50": float(np.median(ctor - entry)) / 1e3,
+                            "copy_fixed_us_p50": float(np.median(copy1 - ctor)) / 1e3,
+                            "copy_live_us_p50": float(np.median(loaded - copy1)) / 1e3,
                             "loop_end_us_p10_p50_p90_max": [float(le[int(q * (B - 1))]) / 1e3 for q in (0.1, .5, .9, 1.0)],
                             "save_us_max": float((saved - loopend).max()) / 1e3,
                             "span_us": (saved.max() - t0) / 1e3})

@@ -20,6 +20,7 @@ PHASES = ["policy", "action", "round_check", "fulfill", "pop", "handle", "post_s
           "#small-table ops", "#big-table ops", "#task launches", "#idle_order"] + [
           f"#decisions {1 << (b + 10)}-{1 << (b + 11)} cycles" for b in range(16)]
 TOP = 8  # the first TOP phases are disjoint; the rest are inclusive sub-timers
+NSTAMPS = 6  # engine.h kTEntry, kTLoaded, kTLoopEnd, kTSaved, kTCtor, kTCopy1
 
 
 def build_prof():
@@ -74,8 +75,8 @@ def main():
     acc = eng.views["acc"]
     d0 = acc[:, _abi.ACC_DECISIONS].sum().item()
     e0 = acc[:, 3].sum().item()
-    # per env: the phase sums, then 4 s_memrealtime stamps (engine.h kTEntry..kTSaved)
-    prof = torch.zeros((B, len(PHASES) + 4), dtype=torch.int64, device=eng.device)
+    # per env: the phase sums, then NSTAMPS s_memrealtime stamps (engine.h kTEntry..kTCopy1)
+    prof = torch.zeros((B, len(PHASES) + NSTAMPS), dtype=torch.int64, device=eng.device)
     lib.ssim_rollout_profiled(eng.handle, _abi.SSIM_POLICY_RANDOM, 1, K, prof.data_ptr(), eng._stream())
     torch.cuda.synchronize()
     d1 = acc[:, _abi.ACC_DECISIONS].sum().item()

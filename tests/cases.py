@@ -286,10 +286,12 @@ def case_sampled_reset(make, dataset, env_cfg, cfg_over, B, seed0, mean_limit):
     assert all(int(v["counts"][i][_abi.OC_ERR]) == 0 for i in range(B))
 
 
-def case_autoreset_replay(make, dataset, env_cfg, B=32, K=1500, mean_limit=None, stride=1):
+def case_autoreset_replay(make, dataset, env_cfg, B=32, K=1500, mean_limit=None, stride=1, budget=0):
     """Fused rollout with SSIM_ROLLOUT_AUTORESET: finished episodes (terminated, or truncated by the time
     limit) restart in place with reset(seed=None). Replaying the logged actions on the oracle, resetting it the
-    same way, reproduces every env's final observation, wall time and episode count."""
+    same way, reproduces every env's final observation, wall time and episode count. budget > 0: the same through
+    the work-conserving ssim_rollout_budget (B*budget decisions shared, at most K per env, no preemption)."""
+    SENT = -99
     cfg = dict(env_cfg, num_executors=4, job_arrival_cap=6, job_arrival_rate=1e-4)
     eng = make(cfg, B, dataset, 0)
     seeds = [7100 + i for i in range(B)]
@@ -297,16 +299,24 @@ def case_autoreset_replay(make, dataset, env_cfg, B=32, K=1500, mean_limit=None,
     opts = None if lim is None else [{"time_limit": float(x)} for x in lim]
     eng.reset(seeds=seeds, options=opts)
     log = eng.alloc_action_log(K)
-    eng.rollout(_abi.SSIM_POLICY_RANDOM, 5, K, log, flags=_abi.SSIM_ROLLOUT_AUTORESET, time_limits=lim)
+    if budget:
+        log.fill_(SENT)
+        eng.rollout_budget(_abi.SSIM_POLICY_RANDOM, 5, K, B * budget, log, flags=_abi.SSIM_ROLLOUT_AUTORESET,
+                           time_limits=lim)
+    else:
+        eng.rollout(_abi.SSIM_POLICY_RANDOM, 5, K, log, flags=_abi.SSIM_ROLLOUT_AUTORESET, time_limits=lim)
     log = np.asarray(eng.to_numpy(log))
     v = eng.host_views()
+    if budget:
+        applied = (log[:, :, 0] != SENT).sum(axis=0)
+        assert applied.sum() == B * budget and applied.max() > applied.min()
     episodes = 0
     for i in range(0, B, stride):
         limit = float("inf") if lim is None else float(lim[i])
         o = SparkSchedOracle(cfg, dataset)
         ob, _ = o.reset(seed=seeds[i], options={"time_limit": limit})
         ep = 1
-        for k in range(K):
+        for k in range(int(applied[i]) if budget else K):
             ob, rew, term, _, info = o.step({"stage_idx": int(log[k, i, 0]), "num_exec": int(log[k, i, 1])})
             if term or info["wall_time"] >= limit:
                 ob, _ = o.reset(seed=None, options={"time_limit": limit})

@@ -80,6 +80,11 @@ def test_autoreset_replay(make, dataset, env_cfg, mean_limit):
     cases.case_autoreset_replay(make, dataset, env_cfg, B=48, K=1500, mean_limit=mean_limit, stride=3)
 
 
+@pytest.mark.parametrize("mean_limit", [None, 2.0e5])
+def test_autoreset_budget_replay(make, dataset, env_cfg, mean_limit):
+    cases.case_autoreset_replay(make, dataset, env_cfg, B=48, K=1500, mean_limit=mean_limit, stride=3, budget=600)
+
+
 def test_async_rollouts(make, dataset, env_cfg):
     cases.case_async_rollouts(make, dataset, env_cfg, device="cuda:0", B=16)
 
