@@ -369,6 +369,9 @@ struct Sim {
   // Requires the header stored (store_header) and in registers (the state after a step or a preemption).
   __device__ __forceinline__ void save_hot() {
     SSIM_TIC(t0);
+#ifdef SSIM_DIAG_NO_SAVE  // diagnostic build only (scripts/build_ab.py): times a launch without its save
+    if (true) return;
+#endif
     if (hot != ghot) {
       const int hi = live_hi();
       const int lo = live_lo < hi ? live_lo : hi;
@@ -1576,10 +1579,10 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- observation (:345-406, utils.py)
-  // Observation-arena stores: written once per decision and never read back by the kernel, so (SSIM_NT_OBS) they
-  // are non-temporal and do not evict the dataset's duration pools from L2.
+  // Observation-arena stores. SSIM_NT_OBS=1 makes them non-temporal (they are never read back by the kernel); measured
+  // on every workload it changed no rate and tripled the HBM write bytes (partial-line streaming writes), so it is off.
 #ifndef SSIM_NT_OBS
-#define SSIM_NT_OBS 1
+#define SSIM_NT_OBS 0
 #endif
   template <class T>
   __device__ __forceinline__ static void obs_st(T* p, T v) {

@@ -32,9 +32,11 @@ for s in "$@"; do
     phase)   step phase 600 python scripts/phase_profile.py ;;
     sweep)   step sweep 900 bash scripts/steps_sweep.sh ;;
     ab)      step ab 900 bash scripts/ab_tpch.sh ;;
+    ab_hbm)  step ab_hbm 1200 bash scripts/ab_hbm.sh ;;
     cpubase) step cpubase 900 python scripts/cpu_baselines.py ;;
     abargs)  step abargs 900 bash scripts/ab_args.sh ;;
     overhead) step overhead 300 python scripts/launch_overhead.py ;;
+    overhead_ab) for lib in gym-sparksched_amd/build/ab/*.so; do n=$(basename "$lib" .so); echo "--- $n"; SSIM_LIB="$PWD/$lib" step "overhead_$n" 300 python scripts/launch_overhead.py; done ;;
     launch)  step launch 600 python scripts/launch_profile.py ;;
     prof_driver) step prof_driver 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_driver" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 ;;
     ab20np)  step ab20np 900 env AB_TAG=s20np AB_ARGS="--steps 20 --warmup 5 --no-preempt" bash scripts/ab_tpch.sh ;;
