@@ -751,15 +751,29 @@ struct Sim {
       i = (i * 5u + 1u + perturb) & mask;
     }
   }
-  __device__ __forceinline__ int lt_load(int p, uint32_t mask) {  // this lane's slot byte (EMPTY past the table)
+  // A pool's metadata and (8-slot table) this lane's slot byte from ONE 16-B record read; tables past 8 slots are
+  // read from the cold block.
+  struct PoolView {
+    uint32_t mask, fill, used;
+    int v;
+  };
+  __device__ __forceinline__ PoolView pool_view(int p) {
+    const PoolRec r = pool(p);
+    uint32_t w[4];
+    __builtin_memcpy(w, &r, sizeof(w));
+    const uint32_t w0 = W::uni(w[0]), w1 = W::uni(w[1]);
+    PoolView pv;
+    pv.mask = w0 & 0xFFFFu;
+    pv.fill = w0 >> 16;
+    pv.used = w1 & 0xFFFFu;
     const int l = W::lane();
-    int v = kSlotEmpty;
-    if (mask == 7) {
-      if (l < 8) v = pool(p).tab[l];
+    if (pv.mask == 7) {
+      const uint64_t tab = ((uint64_t)w[3] << 32) | w[2];
+      pv.v = l < 8 ? (int)((tab >> (8 * l)) & 0xFFu) : kSlotEmpty;
     } else {
-      if (l <= (int)mask) v = ptab(p)[l];
+      pv.v = l <= (int)pv.mask ? (int)ptab(p)[l] : kSlotEmpty;
     }
-    return v;
+    return pv;
   }
   __device__ __forceinline__ void lt_store(int p, uint32_t mask, int slot, int val) {
     W::sync();
@@ -814,8 +828,9 @@ struct Sim {
     lt_meta(p, size - 1, n, n);
   }
   __device__ __forceinline__ void pool_add_lanes(int p, int e) {
-    const uint32_t mask = W::uni(pool(p).mask), fill = W::uni(pool(p).fill), used = W::uni(pool(p).used);
-    const int v = lt_load(p, mask);
+    const PoolView pv = pool_view(p);
+    const uint32_t mask = pv.mask, fill = pv.fill, used = pv.used;
+    const int v = pv.v;
     const uint64_t E = W::ballot(v == kSlotEmpty) & slot_bits(mask), Dm = W::ballot(v == kSlotDummy),
                    K = W::ballot(v == e);
     int empty, dummy;
@@ -833,8 +848,9 @@ struct Sim {
     lt_meta(p, mask, fill + 1, used + 1);
   }
   __device__ __forceinline__ bool pool_remove_lanes(int p, int e) {
-    const uint32_t mask = W::uni(pool(p).mask), fill = W::uni(pool(p).fill), used = W::uni(pool(p).used);
-    const int v = lt_load(p, mask);
+    const PoolView pv = pool_view(p);
+    const uint32_t mask = pv.mask, fill = pv.fill, used = pv.used;
+    const int v = pv.v;
     const uint64_t E = W::ballot(v == kSlotEmpty) & slot_bits(mask), K = W::ballot(v == e);
     int empty, dummy;
     const int slot = lt_probe(E, 0, K, mask, (uint32_t)e, &empty, &dummy);
@@ -868,8 +884,9 @@ struct Sim {
   }
   // idle_order (below) for lane-sized tables: out[0..n) = executor ids, returns n.
   __device__ __forceinline__ int idle_order_lanes(int p, int32_t* out) {
-    const uint32_t mask = W::uni(pool(p).mask), fill = W::uni(pool(p).fill), used = W::uni(pool(p).used);
-    const int v = lt_load(p, mask);
+    const PoolView pv = pool_view(p);
+    const uint32_t mask = pv.mask, fill = pv.fill, used = pv.used;
+    const int v = pv.v;
     const uint64_t occ = W::ballot(v < kSlotDummy) & slot_bits(mask);
     int n = W::popc(occ);
     int kv = W::compact(occ, v);  // keys in table order
@@ -1195,8 +1212,10 @@ struct Sim {
     x.ev_stage = (int16_t)g;
   }
   __device__ __forceinline__ void run_next_task(int e, int g) {  // :584-615
-    StageRec s = ld_rec(stage(g));
-    ExecRec x = ld_rec(exr(e));
+    const StageRec sraw = stage(g);  // both records in one LDS round trip
+    const ExecRec xraw = exr(e);
+    StageRec s = ld_rec(sraw);
+    ExecRec x = ld_rec(xraw);
     run_next_task_rec(g, s, x);
     stage(g) = s;
     exr(e) = x;
@@ -1244,7 +1263,10 @@ struct Sim {
 
   __device__ __forceinline__ void goto_stage(int e, int g) {  // _move_executor_to_stage :799-819 (+ backup loop)
     for (int guard = 0; guard < 4 * SC + 8; ++guard) {
-      if (st_rem(g) == 0) {  // _try_backup_schedule :784-797
+      const StageRec sraw = stage(g);  // the stage record and the executor's job in one LDS round trip
+      const int16_t xjob = exr(e).job;
+      const StageRec sr = ld_rec(sraw);
+      if (sr.rem == 0) {  // _try_backup_schedule :784-797
         const int b = find_backup(e);
         if (b >= 0) {
           g = b;
@@ -1253,12 +1275,12 @@ struct Sim {
         release_idle_one(ex_loc(e), e);
         return;
       }
-      const int j = st_job(g);
-      if (ex_job(e) != j) {
+      const int j = sr.job;
+      if (W::uni(xjob) != j) {
         send(e, g);
         return;
       }
-      if (st_unmet(g) != 0) {  // not in job.frontier_stages
+      if (sr.unmet != 0) {  // not in job.frontier_stages
         ex_task(e) = -1;
         move_to_pool(e, job_pool(j), false);
         return;
@@ -1354,12 +1376,15 @@ struct Sim {
   }
 
   __device__ __forceinline__ void on_executor_arrival(int e, int g) {  // :440-450
-    const int j = st_job(g);
-    check(ex_task(e) < 0);  // Job.attach_executor asserts executor.task is None
+    const StageRec sraw = stage(g);  // stage and executor records in one LDS round trip
+    const ExecRec xraw = exr(e);
+    const StageRec sr = ld_rec(sraw);
+    const int j = sr.job;
+    check(W::uni(xraw.task) < 0);  // Job.attach_executor asserts executor.task is None
     job_local(j) += 1;
     ex_job(e) = (int16_t)j;
-    st_mov(g) -= 1;
-    check(st_mov(g) >= 0);
+    st_mov(g) = (int16_t)(sr.mov - 1);
+    check(sr.mov - 1 >= 0);
     move_to_pool(e, job_pool(j), false);
     goto_stage(e, g);
   }
