@@ -34,7 +34,7 @@ def build_variant(name, defines):
     objs = []
     for tu in VARIANT_TUS:
         obj = os.path.join(objdir, tu + ".o")
-        subprocess.run([G._hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", *defines,
+        subprocess.run([G._hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", *(G.SCHED_FLAGS if tu in G.SCHED_TUS else []), *defines,
                         f"-I{os.path.join(REPO, 'include')}", f"-I{csrc}", "-c", os.path.join(csrc, tu), "-o",
                         obj], check=True)
         objs.append(obj)
