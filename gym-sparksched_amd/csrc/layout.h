@@ -114,6 +114,11 @@ constexpr int kTraceBytes = 32;
 constexpr int64_t kResetHeadBytes = 64;  // ssim_reset_record padded
 static_assert(sizeof(ssim_reset_record) <= kResetHeadBytes, "reset record");
 constexpr int64_t kLdsBudget = 64 * 1024;  // dynamic LDS per workgroup without opt-in
+// Opt-in dynamic LDS of one workgroup on gfx950 (a CU's 160 KB). The LDS-resident engine kernels use it for batches
+// small enough that one env per CU costs nothing (num_envs <= kBigLdsMaxEnvs, one wave per CU), e.g. the 16 envs of a
+// decima_tpch.yaml PPO iteration, whose J=200 / N=50 hot block (~146 KB) otherwise stays in HBM.
+constexpr int64_t kLdsBudgetBig = 160 * 1024;
+constexpr int64_t kBigLdsMaxEnvs = 256;
 
 struct TraceRec {  // one popped event
   double t;
@@ -236,7 +241,8 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
   L->state_bytes = 4096 + L->env_bytes * B;  // params block (engine.h kParamsReserve) + env blocks
   L->scratch_bytes = O->scratch_bytes;
   // LDS per wave: [hot copy (if resident) | scratch]
-  O->lds_resident = (O->hot_bytes + O->scratch_bytes <= kLdsBudget) ? 1 : 0;
+  const int64_t need = O->hot_bytes + O->scratch_bytes;
+  O->lds_resident = (need <= kLdsBudget || (need <= kLdsBudgetBig && B <= kBigLdsMaxEnvs)) ? 1 : 0;
   O->lds_bytes = O->scratch_bytes + (O->lds_resident ? O->hot_bytes : 0);
 
   // obs arena: each field is [B][per-env]

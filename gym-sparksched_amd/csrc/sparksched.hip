@@ -136,6 +136,14 @@ static int hip_check(hipError_t e, const char* what) {
   return SSIM_OK;
 }
 
+// A launch with more than 64 KB of dynamic LDS (layout.h kLdsBudgetBig) needs the kernel's opt-in attribute. It is
+// per-device state, so it is set before every such launch (idempotent; only small batches take this path).
+static int lds_opt_in(const void* fn, int64_t lds) {
+  if (lds <= kLdsBudget) return SSIM_OK;
+  return hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                   "engine kernel LDS attribute");
+}
+
 extern "C" int ssim_layout_for(const ssim_config* cfg, ssim_layout* out) {
   StateOffsets O;
   if (cfg == nullptr || out == nullptr || !compute_layout(*cfg, out, &O))
@@ -153,7 +161,7 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
     delete h;
     return set_err(SSIM_E_ARG, "ssim_create: invalid config");
   }
-  if (h->params.O.lds_bytes > kLdsBudget) {
+  if (h->params.O.lds_bytes > (h->params.O.lds_resident ? kLdsBudgetBig : kLdsBudget)) {
     delete h;
     return set_err(SSIM_E_ARG, "ssim_create: per-env scratch %lld B exceeds the LDS budget",
                    (long long)h->params.O.lds_bytes);
@@ -214,7 +222,10 @@ extern "C" int ssim_reset(ssim_handle* h, void* stream) {
 extern "C" int ssim_step(ssim_handle* h, const int32_t* stage_idx, const int32_t* num_exec, void* stream) {
   if (h == nullptr || stage_idx == nullptr || num_exec == nullptr) return set_err(SSIM_E_ARG, "ssim_step: null");
   const ssim_layout& L = h->params.L;
-  hipLaunchKernelGGL(pick_step(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+  const StepFn fn = pick_step(h->params);
+  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  if (rc != SSIM_OK) return rc;
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, stage_idx, num_exec);
   return hip_check(hipGetLastError(), "k_step launch");
 }
@@ -243,11 +254,14 @@ static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t n
   if ((flags & SSIM_ROLLOUT_AUTORESET) && !(h->params.C.job_arrival_gap > 0.0))
     return set_err(SSIM_E_ARG, "ssim_rollout_ex: auto-reset needs job_arrival_gap in the config");
   const ssim_layout& L = h->params.L;
+  const RolloutFn fn = pick_rollout(h->params, (flags & SSIM_ROLLOUT_WARMUP) != 0);
+  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  if (rc != SSIM_OK) return rc;
   if (budget > 0) {
     if (h->ticket_slot) flags |= kFlagTicketSlot;
     h->ticket_slot ^= 1;
   }
-  hipLaunchKernelGGL(pick_rollout(h->params, (flags & SSIM_ROLLOUT_WARMUP) != 0), dim3(L.num_envs), dim3(64),
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64),
                      (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, flags, time_limits, h->reset, action_log,
                      (uint64_t*)nullptr, budget, env_steps);
