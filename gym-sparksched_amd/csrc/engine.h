@@ -369,9 +369,6 @@ struct Sim {
   // Requires the header stored (store_header) and in registers (the state after a step or a preemption).
   __device__ __forceinline__ void save_hot() {
     SSIM_TIC(t0);
-#ifdef SSIM_DIAG_NO_SAVE  // diagnostic build only (scripts/build_ab.py): times a launch without its save
-    if (true) return;
-#endif
     if (hot != ghot) {
       const int hi = live_hi();
       const int lo = live_lo < hi ? live_lo : hi;
