@@ -523,7 +523,8 @@ struct Sim {
   }
   __device__ __forceinline__ int committable() {  // :105-111 (pool None is always empty with no commitments)
     if (h.source < 0) return 0;
-    const int n = pool_size(h.source) - cfrom(h.source);
+    const PoolRec pr = pool(h.source);  // size and commitments-from in one LDS round trip
+    const int n = (int)W::uni(pr.used) - (int)W::uni(pr.cfrom);
     check(n >= 0);
     return n;
   }

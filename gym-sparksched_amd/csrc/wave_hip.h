@@ -88,26 +88,32 @@ struct WaveHip {
   // wave the four row minima are combined on the scalar side. All 64 lanes must be active (callers run in
   // wave-uniform control flow).
   template <int kCtrl>
-  __device__ static __forceinline__ double dpp_d(double v) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)b, (int)(uint32_t)b, kCtrl, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(b >> 32), (int)(uint32_t)(b >> 32), kCtrl, 0xF, 0xF,
-                                               false);
-    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  __device__ static __forceinline__ uint64_t dpp_u(uint64_t b) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, kCtrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), kCtrl, 0xF, 0xF, false);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
   }
+  __device__ static __forceinline__ uint64_t umin(uint64_t a, uint64_t b) { return b < a ? b : a; }
+  // Event times are non-negative doubles or +inf, whose bit patterns order like unsigned integers: the min runs on
+  // the bits (no canonicalising f64 min).
   template <int kSpan>
   __device__ static __forceinline__ double min_d(double v) {
-    v = __builtin_fmin(v, dpp_d<0xB1>(v));   // quad_perm [1,0,3,2]
-    v = __builtin_fmin(v, dpp_d<0x4E>(v));   // quad_perm [2,3,0,1]
-    v = __builtin_fmin(v, dpp_d<0x124>(v));  // row_ror:4
-    v = __builtin_fmin(v, dpp_d<0x128>(v));  // row_ror:8
-    double m = bcast_d(v, 0);
+    uint64_t b = __builtin_bit_cast(uint64_t, v);
+    b = umin(b, dpp_u<0xB1>(b));   // quad_perm [1,0,3,2]
+    b = umin(b, dpp_u<0x4E>(b));   // quad_perm [2,3,0,1]
+    b = umin(b, dpp_u<0x124>(b));  // row_ror:4
+    b = umin(b, dpp_u<0x128>(b));  // row_ror:8
+    uint64_t m = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 0) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 0) << 32);
     if (kSpan > 16) {
-      const double m1 = bcast_d(v, 16), m2 = bcast_d(v, 32), m3 = bcast_d(v, 48);
-      m = __builtin_fmin(__builtin_fmin(m, m1), __builtin_fmin(m2, m3));
+      for (int r = 16; r < 64; r += 16) {
+        const uint64_t mr = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, r) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), r) << 32);
+        m = umin(m, mr);
+      }
       m = uni(m);
     }
-    return m;
+    return __builtin_bit_cast(double, m);
   }
   // Argmin of (t, seq) over lanes [0, kSpan) with `valid`: the winning lane (-1 if none). One DPP min of t,
   // then the (rare) ties on t are broken by the smaller seq. `tmin` receives the winning t.
