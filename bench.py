@@ -135,7 +135,7 @@ def _cpu_worker(args):
     """One reference-style rollout worker (trainers/rollout_worker.py:53-95): one env per process, single
     thread, episodes back to back with the workload's policy; warm-up = the first episode (at most
     `warm_s` seconds), then decisions are counted for `seconds` of wall time."""
-    workload, seed, seconds, warm_s = args
+    workload, seed, seconds, warm_s, ds_seed = args
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "gym-sparksched_amd"))
     import numpy as np
@@ -153,7 +153,7 @@ def _cpu_worker(args):
         torch = None
     wl = _workload(workload)
     cfg = wl["cfg"]
-    env = SparkSchedOracle(cfg, generate(0))
+    env = SparkSchedOracle(cfg, generate(ds_seed))
     if wl["mean_time_limit"]:
         env = StochasticTimeLimit(env, wl["mean_time_limit"])
     if wl["policy"] == "decima":
@@ -203,13 +203,13 @@ def _cpu_worker(args):
     return decisions, time.perf_counter() - t0, episodes
 
 
-def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0) -> dict:
+def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0, ds_seed: int = 0) -> dict:
     """The reference's CPU rollout path, timed on this host's cores: the oracle restatement (same CPython
     dict/set/heapq and numpy Generator machinery as spark_sched_sim) in `procs` spawn processes, one env each,
     harness shaped like trainers/rollout_worker.py:53-95."""
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(workload, 7 + i, seconds, warm_s) for i in range(procs)])
+        res = pool.map(_cpu_worker, [(workload, 7 + i, seconds, warm_s, ds_seed) for i in range(procs)])
     dec = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     host = os.cpu_count() or procs
@@ -228,7 +228,8 @@ def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0)
 
 
 # ------------------------------------------------------------------------------------------------ PMC lookup
-def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisions_per_launch: float):
+def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisions_per_launch: float,
+                dataset_seed: int = 0):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*/pmc_summary*.json,
     made by scripts/pmc_profile.sh + scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
     separate passes), scaled from bytes/decision to this launch; plus the summary's issue counters per decision
@@ -244,7 +245,7 @@ def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisi
         cfg = k.get("config") or {}
         spl = cfg.get("steps_per_launch", k.get("steps") if mode == "rollout" else 1)
         if (cfg.get("mode") == mode and cfg.get("envs_per_gpu") == envs and spl == steps_per_launch
-                and "hbm_bytes_per_decision" in k):
+                and cfg.get("dataset_seed", 0) == dataset_seed and "hbm_bytes_per_decision" in k):
             best = (path, k)
     if best is None:
         return None, None, None
@@ -334,6 +335,10 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = every usable CPU of this job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--dataset-seed", type=int, default=0,
+                    help="synthetic TPC-H-format dataset generator seed (0: stage cap 900, the bench kernel with every "
+                         "shape constant; 1: stage cap 850, the kernel that reads the cap at run time, as real "
+                         "traces would)")
     ap.add_argument("--torch-policy", action="store_true",
                     help="decima workload: run the PyTorch DecimaScheduler instead of the fused kernel")
     ap.add_argument("--ppo-time-limit", type=float, default=0.0,
@@ -391,12 +396,12 @@ def main():
         sys.path.insert(0, os.path.join(REPO, "tests", "hostsim"))
         from driver import HostEngine  # TEST-ONLY host build (see --engine)
 
-        eng = HostEngine(cfg, B, generate(0))
+        eng = HostEngine(cfg, B, generate(args.dataset_seed))
         args.lockstep = True  # the host build has no shared-budget launch
     else:
         from spark_sched_sim.engine import DeviceEngine
 
-        eng = DeviceEngine(cfg, B, generate(0), device=dev)
+        eng = DeviceEngine(cfg, B, generate(args.dataset_seed), device=dev)
     seeds = shard_seeds(rank, B, args.seed)
     limits = None
     if wl["mean_time_limit"]:  # StochasticTimeLimit (wrappers/stochastic_time_limit.py:5-31), per env
@@ -528,7 +533,7 @@ def main():
             kern_ms = kern_ms_sum / world
             achieved = (alg_bytes / world / launches) / (kern_ms / launches / 1e3) / 1e9  # GB/s per GPU
             traffic, traffic_src, pmc = pmc_traffic(kernel, mode, B, K if mode == "rollout" else 1,
-                                                   decisions / world / launches)
+                                                   decisions / world / launches, args.dataset_seed)
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                         "kernel": kernel, "kernel_ms_per_launch": kern_ms / launches,
@@ -564,7 +569,12 @@ def main():
                        if mode == "rollout" else None,
                        "preroll": {"bound": preroll, "mean_decisions": float(pre_steps.mean())},
                        "autoreset": bool(mode != "step" and (flags or mode == "decima")),
-                       "parallelism": f"env-sharded x{world}"},
+                       "parallelism": f"env-sharded x{world}",
+                       "dataset": {"generator": "synthetic_tpch", "seed": args.dataset_seed,
+                                   "stage_cap": int(eng.layout.stage_cap),
+                                   "kernel": ("shape-specialised (stage cap 900)" if int(eng.layout.stage_cap) == 900
+                                              and cfg["num_executors"] == 10 and cfg["job_arrival_cap"] == 50
+                                              else "stage cap read at run time")}},
             "decisions": int(decisions),
             "episodes_finished": int(episodes_done),
             "events_per_decision": events_sum / max(decisions, 1.0),
@@ -581,7 +591,7 @@ def main():
             line["engine"] = "hostsim (TEST-ONLY CPU build; not a measurement)"
         if not args.no_cpu_baseline and world == 1 and not host and args.workload in ("tpch", "large", "decima"):
             procs = args.cpu_procs or usable_cpus()
-            line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, procs)
+            line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, procs, ds_seed=args.dataset_seed)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -24,10 +24,12 @@
 #include "pcg64.h"
 #include "pyset.h"
 
-// Diagnostic build only (-DSSIM_PROFILE, scripts/phase_profile.py): per-phase shader-clock sums per wave.
+// Diagnostic build only (-DSSIM_PROFILE, scripts/phase_profile.py): per-phase shader-clock sums per wave, kept in
+// a small LDS area of the wave's scratch block (StateOffsets::sc_prof) and added to by lane 0 with no-return LDS
+// atomics, so a timer costs no register array (no scratch memory) and no dependent round trip.
 #ifdef SSIM_PROFILE
 #define SSIM_TIC(v) const uint64_t v = W::clock()
-#define SSIM_TOC(v, ph) prof[ph] += W::clock() - (v)
+#define SSIM_TOC(v, ph) prof_add(ph, W::clock() - (v))
 #else
 #define SSIM_TIC(v) (void)0
 #define SSIM_TOC(v, ph) (void)0
@@ -65,6 +67,8 @@ __device__ __forceinline__ T ldg(const T* p, int64_t i) {
 enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kPhHandle, kPhPostScan, kPhObserve,
                  kPhSample, kPhPool, kPhScan, kPhLoadSave, kPhPoolBig, kPhIdleOrder, kPhDraw, kPhJobArr,
                  kPhExecArr, kPhTaskDone, kPhStageDone,
+                 // whole loop iterations of the rollout (policy + step, or completing a pending step, or an auto-reset)
+                 kPhIter,
                  // event counters (not cycles)
                  kCtPoolSmall, kCtPoolBig, kCtTask, kCtIdleOrder,
                  // histogram of whole-decision cycles (policy + step + auto-reset): bucket b = [2^(b+10), 2^(b+11))
@@ -73,7 +77,7 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
                  // constructed, fixed sections copied
                  kTEntry = kHist0 + 16, kTLoaded, kTLoopEnd, kTSaved, kTCtor, kTCopy1, kNumPhases };
 #ifdef SSIM_PROFILE
-#define SSIM_COUNT(ph) prof[ph] += 1
+#define SSIM_COUNT(ph) prof_add(ph, 1)
 #else
 #define SSIM_COUNT(ph) (void)0
 #endif
@@ -232,7 +236,15 @@ struct Sim {
   const HotParams* HPp;  // host build: Params::hp read in place
   uint32_t hpv;          // device: dword `lane` of Params::hp
 #ifdef SSIM_PROFILE
-  uint64_t prof[kNumPhases] = {0};
+  uint64_t* prof;  // LDS: kNumPhases sums of this wave (lane 0 adds)
+  __device__ __forceinline__ void prof_add(int ph, uint64_t v) {
+    if (W::lane() == 0) W::lds_add_u64(prof + ph, v);
+  }
+  __device__ __forceinline__ void prof_set(int ph, uint64_t v) {
+    W::sync();
+    if (W::lane() == 0) prof[ph] = v;
+    W::sync();
+  }
 #endif
 
   // `lds` = this wave's LDS block: [hot copy (if resident) | scratch]; resident=false keeps hot in HBM.
@@ -248,6 +260,11 @@ struct Sim {
     HPp = &p->hp;
     hpv = (W::kWidth == 64 && W::lane() < (int)(sizeof(HotParams) / 4)) ? reinterpret_cast<const uint32_t*>(&p->hp)[W::lane()]
                                                                       : 0u;
+#ifdef SSIM_PROFILE
+    prof = reinterpret_cast<uint64_t*>(scr + O.sc_prof);
+    for (int i = W::lane(); i < kNumPhases; i += W::kWidth) prof[i] = 0;
+    W::sync();
+#endif
   }
   // A HotParams field: v_readlane of hpv on device (constant lanes), the field itself in the host build.
   template <class T, int kOff>
@@ -265,6 +282,10 @@ struct Sim {
       return host_val;
     }
   }
+// HP() reads other lanes of `hpv`, so it is only ever evaluated in wave-uniform control flow (all 64 lanes
+// active): a VGPR reloaded from a spill under a partial EXEC mask holds garbage in its inactive lanes. Lane-parallel
+// loops and lane-0 blocks take the fields they need as locals hoisted in front of them (TopoView, the observe() and
+// trace() pointers, ...); the locals are SGPRs, whose spills go to whole-wave VGPR lanes.
 #define HP(f) hp_get<decltype(HotParams::f), (int)offsetof(HotParams, f)>(HPp->f)
 
   // ---------------------------------------------------------------- hot-block residency
@@ -294,7 +315,7 @@ struct Sim {
         int64_t o = -1;
 #pragma unroll
         for (int r = kSpans - 1; r >= 0; --r)
-          if (i < end[r]) o = sp[r].off + ((i - (end[r] - sp[r].n)) << 4);
+          if (i < end[r]) o = sp[r].off + (i - (end[r] - sp[r].n)) * 16;  // (a later r overwrites: may be < 0)
         at[u] = i < total ? o : -1;
         if (at[u] >= 0) v[u] = *reinterpret_cast<const uint4*>(src + at[u]);
       }
@@ -321,7 +342,7 @@ struct Sim {
       const Span fixed[2] = {{0, O.stages >> 4}, {O.pools, 1 + JC}};
       copy_spans(hot, ghot, fixed);
 #ifdef SSIM_PROFILE
-      prof[kTCopy1] = __builtin_amdgcn_s_memrealtime();
+      prof_set(kTCopy1, W::realtime());
 #endif
       load_header();
       // lowest stage still referenced (jobs' stages are contiguous in arrival order): the stages of the active
@@ -1002,9 +1023,11 @@ struct Sim {
   }
 
   __device__ __forceinline__ void trace(double t, int kind, int e, int job, int sid, int seq) {
-    if (HP(trace_cap) == 0) return;  // tracing off: no bookkeeping at all
-    if (h.trace_len < HP(trace_cap) && W::lane() == 0) {
-      TraceRec* r = reinterpret_cast<TraceRec*>(obs + HP(ob_trace)) + (int64_t)eid * HP(trace_cap) + h.trace_len;
+    const int cap = HP(trace_cap);
+    if (cap == 0) return;  // tracing off: no bookkeeping at all
+    TraceRec* const base = reinterpret_cast<TraceRec*>(obs + HP(ob_trace)) + (int64_t)eid * cap;
+    if (h.trace_len < cap && W::lane() == 0) {
+      TraceRec* r = base + h.trace_len;
       r->t = t;
       r->kind = kind;
       r->exec = e;
@@ -1026,11 +1049,13 @@ struct Sim {
   __device__ __forceinline__ DurDesc dur_gather(int ts) const {
     DurDesc d{0, 0};
     if (W::kWidth >= 24) {
+      const int32_t* const dlen = HP(dur_len);  // (uniform reads, before the lane-divergent loads)
+      const int32_t* const doff = HP(dur_off);
       const int l = W::lane();
       if (l < 24) {
         const int idx = (ts * 3 + (l >> 3)) * kNumLevels + (l & 7);
-        d.len = ldg(HP(dur_len), idx);
-        d.off = ldg(HP(dur_off), idx);
+        d.len = ldg(dlen, idx);
+        d.off = ldg(doff, idx);
       }
     }
     return d;
@@ -1093,7 +1118,25 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- schedulable-stage search (:505-555)
-  __device__ __forceinline__ bool stage_pred(int g, int mode, int jx, int src_job) const {
+  // The dataset's DAG tables, read from HP in uniform control flow by the callers of the lane-parallel predicates.
+  struct TopoView {
+    const uint64_t* ts_topo;
+    const int32_t *parent_base, *parents, *child_base, *children;
+    bool bits;  // templates of <= 32 stages: parents / children as bit sets (ts_topo)
+  };
+  __device__ __forceinline__ TopoView topo_view() const {
+    TopoView v{nullptr, nullptr, nullptr, nullptr, nullptr, HP(topo) != 0};
+    if (v.bits) {  // (a uniform branch: only the tables the path uses are read)
+      v.ts_topo = HP(ts_topo);
+    } else {
+      v.parent_base = HP(ts_parent_base);
+      v.parents = HP(ts_parents);
+      v.child_base = HP(ts_child_base);
+      v.children = HP(ts_children);
+    }
+    return v;
+  }
+  __device__ __forceinline__ bool stage_pred(int g, int mode, int jx, int src_job, const TopoView& tv) const {
     const StageRec s = stage(g);  // one 16-B record read
     const int j = s.job;
     if (mode == kScanOnly && j != jx) return false;
@@ -1103,8 +1146,8 @@ struct Sim {
     if (s.sel) return false;
     if (s.rem - (s.mov + s.com) <= 0) return false;
     const int base = jr.base;
-    if (topo_masks()) {  // one dataset load for all parents, then their records
-      uint32_t pm = (uint32_t)ldg(HP(ts_topo), s.ts);
+    if (tv.bits) {  // one dataset load for all parents, then their records
+      uint32_t pm = (uint32_t)ldg(tv.ts_topo, s.ts);
       while (pm) {
         const StageRec ps = stage(base + __builtin_ctz(pm));
         pm &= pm - 1;
@@ -1112,8 +1155,8 @@ struct Sim {
       }
       return true;
     }
-    for (int k = ldg(HP(ts_parent_base), s.ts); k < ldg(HP(ts_parent_base), s.ts + 1); ++k) {
-      const StageRec ps = stage(base + ldg(HP(ts_parents), k));
+    for (int k = ldg(tv.parent_base, s.ts); k < ldg(tv.parent_base, s.ts + 1); ++k) {
+      const StageRec ps = stage(base + ldg(tv.parents, k));
       if (ps.rem - (ps.mov + ps.com) > 0) return false;
     }
     return true;
@@ -1127,11 +1170,12 @@ struct Sim {
     SSIM_TIC(t0);
     const int n = h.n_active_stages;
     const int16_t* act = H<int16_t>(O.active_stages);
+    const TopoView tv = topo_view();
     int found = -1;
     for (int i0 = 0; i0 < n; i0 += W::kWidth) {
       const int i = i0 + W::lane();
       const int g = i < n ? act[i] : -1;
-      const uint64_t m = W::ballot(g >= 0 && stage_pred(g, mode, jx, src_job));
+      const uint64_t m = W::ballot(g >= 0 && stage_pred(g, mode, jx, src_job, tv));
       if (m) {
         found = W::bcast_i(g, W::ffs(m));
         break;
@@ -1342,6 +1386,11 @@ struct Sim {
     int16_t* as = H<int16_t>(O.active_stages);
     if (W::lane() == 0) aj[h.n_active_jobs] = (int16_t)j;
     const int base = job_base(j), n = job_nst(j), tsb = ldu(HP(tpl_stage_base), (int)job_tpl(j));
+    const int32_t* const nt = HP(ts_num_tasks);  // (uniform reads, before the lane-divergent block)
+    const int32_t* const pb = HP(ts_parent_base);
+    const int32_t* const fwk = HP(ts_fw_keymask);
+    const int32_t* const fwm = HP(ts_fw_maxlevel);
+    const double* const rough = HP(ts_rough);
     for (int k0 = 0; k0 <= n; k0 += W::kWidth) {  // stage records, pools of the job and its stages, active list
       const int k = k0 + W::lane();
       if (k <= n) {
@@ -1353,16 +1402,16 @@ struct Sim {
           StageRec r;
           r.job = (int16_t)j;
           r.ts = (int16_t)ts;
-          r.rem = (int16_t)ldg(HP(ts_num_tasks), ts);
+          r.rem = (int16_t)ldg(nt, ts);
           r.exe = 0;
           r.mov = 0;
           r.com = 0;
-          r.unmet = (int8_t)(ldg(HP(ts_parent_base), ts + 1) - ldg(HP(ts_parent_base), ts));
+          r.unmet = (int8_t)(ldg(pb, ts + 1) - ldg(pb, ts));
           r.sel = 0;
-          r.fw_keymask = (uint8_t)ldg(HP(ts_fw_keymask), ts);
-          r.fw_maxlevel = (uint8_t)ldg(HP(ts_fw_maxlevel), ts);
+          r.fw_keymask = (uint8_t)ldg(fwk, ts);
+          r.fw_maxlevel = (uint8_t)ldg(fwm, ts);
           stage(g) = r;
-          recent()[g] = ldg(HP(ts_rough), ts);
+          recent()[g] = ldg(rough, ts);
           as[h.n_active_stages + k] = (int16_t)g;
         }
       }
@@ -1583,6 +1632,7 @@ struct Sim {
     const double span = h.wall - t0;
     if (span == 0.0) return 0.0;
     double part = 0.0;
+    const double beta = HP(beta);
     for (int j0 = 0; j0 < h.arrivals; j0 += W::kWidth) {
       const int j = j0 + W::lane();
       if (j < h.arrivals) {
@@ -1595,15 +1645,15 @@ struct Sim {
           const double a = ta > t0 ? ta : t0;
           const double tc = st == kJobDone ? jt.tdone : h.wall;
           const double b = tc < h.wall ? tc : h.wall;
-          if (HP(beta) == 0.0)
+          if (beta == 0.0)
             part += b - a;
           else
-            part += exp(-HP(beta) * 1e-3 * (a - t0)) - exp(-HP(beta) * 1e-3 * (b - t0));
+            part += exp(-beta * 1e-3 * (a - t0)) - exp(-beta * 1e-3 * (b - t0));
         }
       }
     }
     double total = W::sum_d(part);
-    if (HP(beta) > 0.0) total /= HP(beta);
+    if (beta > 0.0) total /= beta;
     return total;
   }
 
@@ -1629,6 +1679,8 @@ struct Sim {
     float* nodes = reinterpret_cast<float*>(obs + HP(ob_nodes)) + (int64_t)eid * SC * 3;
     uint8_t* front = obs + HP(ob_frontier) + (int64_t)eid * SC;
     int32_t* srank = reinterpret_cast<int32_t*>(obs + HP(ob_sched_rank)) + (int64_t)eid * SC;
+    const TopoView tv = topo_view();
+    const int ecap = HP(edge_cap);
     // picks[j] (job id j): heuristics/utils.py find_stage of the job, packed as a min key over its
     // schedulable nodes: (frontier ? 0 : 1 << 16) | schedulable rank; INT32_MAX = none. Nodes of a job are
     // contiguous in node order and ranks grow with node order, so the min is the first frontier stage,
@@ -1645,7 +1697,7 @@ struct Sim {
       const int i = i0 + W::lane();
       const bool ok = i < n;
       const int g = ok ? act[i] : -1;
-      const bool s = ok && stage_pred(g, kScanAll, -1, src_job);
+      const bool s = ok && stage_pred(g, kScanAll, -1, src_job, tv);
       const uint64_t m = W::ballot(s);
       const int r = nsched + W::rank(m);
       if (ok) {
@@ -1689,7 +1741,7 @@ struct Sim {
     if (W::lane() == 0) obs_st(ptr + nj, run);
     check(run == n);
     // edges: (row(u), row(v)) for active u, child v active; order = node order, children ascending
-    int64_t* links = reinterpret_cast<int64_t*>(obs + HP(ob_edge_links)) + (int64_t)eid * HP(edge_cap) * 2;
+    int64_t* links = reinterpret_cast<int64_t*>(obs + HP(ob_edge_links)) + (int64_t)eid * ecap * 2;
     int ne = 0;
     for (int i0 = 0; i0 < n; i0 += W::kWidth) {
       const int i = i0 + W::lane();
@@ -1700,8 +1752,8 @@ struct Sim {
       if (ok) {
         const StageRec sr = stage(g);
         base = job(sr.job).base;
-        if (topo_masks()) {
-          uint32_t cm = (uint32_t)(ldg(HP(ts_topo), sr.ts) >> 32);
+        if (tv.bits) {
+          uint32_t cm = (uint32_t)(ldg(tv.ts_topo, sr.ts) >> 32);
           while (cm) {
             const int b = __builtin_ctz(cm);
             cm &= cm - 1;
@@ -1710,10 +1762,10 @@ struct Sim {
           }
           cnt = __builtin_popcount(live);
         } else {
-          cb = ldg(HP(ts_child_base), sr.ts);
-          ce = ldg(HP(ts_child_base), sr.ts + 1);
+          cb = ldg(tv.child_base, sr.ts);
+          ce = ldg(tv.child_base, sr.ts + 1);
           for (int k = cb; k < ce; ++k) {
-            const StageRec c = stage(base + ldg(HP(ts_children), k));
+            const StageRec c = stage(base + ldg(tv.children, k));
             if (!(c.rem == 0 && c.exe == 0)) cnt++;
           }
         }
@@ -1722,8 +1774,8 @@ struct Sim {
       const int ex = W::excl_scan(cnt, &total);
       if (ok) {
         int o = ne + ex;
-        if (topo_masks()) {
-          while (live && o < HP(edge_cap)) {
+        if (tv.bits) {
+          while (live && o < ecap) {
             const int c = base + __builtin_ctz(live);
             live &= live - 1;
             obs_st(links + 2 * o + 0, (int64_t)i);
@@ -1732,9 +1784,9 @@ struct Sim {
           }
         } else {
           for (int k = cb; k < ce; ++k) {
-            const int c = base + ldg(HP(ts_children), k);
+            const int c = base + ldg(tv.children, k);
             const StageRec cr = stage(c);
-            if (!(cr.rem == 0 && cr.exe == 0) && o < HP(edge_cap)) {
+            if (!(cr.rem == 0 && cr.exe == 0) && o < ecap) {
               obs_st(links + 2 * o + 0, (int64_t)i);
               obs_st(links + 2 * o + 1, (int64_t)row_of[c]);
               o++;
@@ -1744,7 +1796,7 @@ struct Sim {
       }
       ne += total;
     }
-    if (ne > HP(edge_cap)) fail(SSIM_ERR_CAPACITY);
+    if (ne > ecap) fail(SSIM_ERR_CAPACITY);
     h.n_sched = nsched;
     h.src_idx = src_idx;
     h.stage_idx_n = n + 1;
@@ -1754,9 +1806,13 @@ struct Sim {
     a.jobs += nj;
     a.events += h.step_events;
     *H<EnvAcc>(O.acc) = a;
+    int64_t* const acc = reinterpret_cast<int64_t*>(obs + HP(ob_acc)) + (int64_t)eid * kNumAcc;
+    int32_t* const cnts = reinterpret_cast<int32_t*>(obs + HP(ob_counts)) + (int64_t)eid * SSIM_NUM_COUNTS;
+    double* const rew = reinterpret_cast<double*>(obs + HP(ob_reward)) + eid;
+    double* const wall = reinterpret_cast<double*>(obs + HP(ob_wall_time)) + eid;
+    const int ncommit = committable();
     W::sync();
     if (W::lane() == 0) {
-      int64_t* acc = reinterpret_cast<int64_t*>(obs + HP(ob_acc)) + (int64_t)eid * kNumAcc;
       acc[0] = a.nodes;
       acc[1] = a.edges;
       acc[2] = a.jobs;
@@ -1765,11 +1821,10 @@ struct Sim {
       acc[5] = a.episodes;
       acc[6] = 0;
       acc[7] = 0;
-      int32_t* cnts = reinterpret_cast<int32_t*>(obs + HP(ob_counts)) + (int64_t)eid * SSIM_NUM_COUNTS;
       cnts[SSIM_OC_NUM_NODES] = n;
       cnts[SSIM_OC_NUM_EDGES] = ne;
       cnts[SSIM_OC_NUM_JOBS] = nj;
-      cnts[SSIM_OC_COMMITTABLE] = committable();
+      cnts[SSIM_OC_COMMITTABLE] = ncommit;
       cnts[SSIM_OC_SOURCE_JOB_IDX] = src_idx;
       cnts[SSIM_OC_NUM_SCHEDULABLE] = nsched;
       cnts[SSIM_OC_TERMINATED] = h.terminated;
@@ -1782,16 +1837,16 @@ struct Sim {
       cnts[SSIM_OC_TRACE_LEN] = h.trace_len;
       cnts[SSIM_OC_STEP_EVENTS] = h.step_events;
       cnts[SSIM_OC_EPISODE] = h.episode;
-      reinterpret_cast<double*>(obs + HP(ob_reward))[eid] = reward;
-      reinterpret_cast<double*>(obs + HP(ob_wall_time))[eid] = h.wall;
+      *rew = reward;
+      *wall = h.wall;
     }
     W::sync();
   }
 
   __device__ __forceinline__ void write_err_only(uint32_t transient) {
+    int32_t* const cnts = reinterpret_cast<int32_t*>(obs + HP(ob_counts)) + (int64_t)eid * SSIM_NUM_COUNTS;
     W::sync();
     if (W::lane() == 0) {
-      int32_t* cnts = reinterpret_cast<int32_t*>(obs + HP(ob_counts)) + (int64_t)eid * SSIM_NUM_COUNTS;
       cnts[SSIM_OC_ERR] = (int32_t)(h.err | transient);
     }
     W::sync();
@@ -2023,12 +2078,14 @@ struct Sim {
     // jobs: template, stage base (exclusive scan of stage counts)
     int run = 0;
     bool bad = false;
+    const int ntpl = HP(num_templates);
+    const int32_t* const tsb = HP(tpl_stage_base);
     for (int j0 = 0; j0 < nj; j0 += W::kWidth) {
       const int j = j0 + W::lane();
       const bool ok = j < nj;
       const int t = ok ? tpl[j] : 0;
-      const bool tb = ok && (t < 0 || t >= HP(num_templates));
-      const int ns = (ok && !tb) ? ldg(HP(tpl_stage_base), t + 1) - ldg(HP(tpl_stage_base), t) : 0;
+      const bool tb = ok && (t < 0 || t >= ntpl);
+      const int ns = (ok && !tb) ? ldg(tsb, t + 1) - ldg(tsb, t) : 0;
       int total = 0;
       const int ex = W::excl_scan(ns, &total);
       if (ok) {

@@ -109,16 +109,16 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
   const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   if (!autoreset && action_log == nullptr && env_idle(P, state, eid)) return;
 #ifdef SSIM_PROFILE
-  const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime();
+  const uint64_t rt_entry = WaveHip::realtime();
 #endif
   Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
 #ifdef SSIM_PROFILE
-  s.prof[kTCtor] = __builtin_amdgcn_s_memrealtime();
+  s.prof_set(kTCtor, WaveHip::realtime());
 #endif
   s.load_hot();
 #ifdef SSIM_PROFILE
-  s.prof[kTEntry] = rt_entry;
-  s.prof[kTLoaded] = __builtin_amdgcn_s_memrealtime();
+  s.prof_set(kTEntry, rt_entry);
+  s.prof_set(kTLoaded, WaveHip::realtime());
 #endif
   // Shared budget (budget > 0): decisions are claimed from one device counter in chunks sized to what is
   // left (guided self-scheduling: 8 early, 1 at the end), so the launch ends within ~one decision of the
@@ -164,7 +164,7 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
       }
       const StepIn a = sim_policy(s, kind, seed);
 #ifdef SSIM_PROFILE
-      s.prof[kPhPolicy] += WaveHip::clock() - t0;
+      s.prof_add(kPhPolicy, WaveHip::clock() - t0);
 #endif
       if (action_log != nullptr && WaveHip::lane() == 0) {
         action_log[((int64_t)k * B + eid) * 2 + 0] = a.stage_idx;
@@ -180,18 +180,20 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
       const uint64_t dc = WaveHip::clock() - t0;
       int b = 63 - __builtin_clzll(dc | 1ull) - 10;
       b = b < 0 ? 0 : b > 15 ? 15 : b;
-      s.prof[kHist0 + b] += 1;
+      s.prof_add(kHist0 + b, 1);
+      s.prof_add(kPhIter, dc);
     }
 #endif
   }
 #ifdef SSIM_PROFILE
-  s.prof[kTLoopEnd] = __builtin_amdgcn_s_memrealtime();
+  s.prof_set(kTLoopEnd, WaveHip::realtime());
 #endif
   s.save_hot();
 #ifdef SSIM_PROFILE
-  s.prof[kTSaved] = __builtin_amdgcn_s_memrealtime();
-  if (prof_out != nullptr && WaveHip::lane() == 0)
-    for (int p = 0; p < kNumPhases; ++p) prof_out[(int64_t)eid * kNumPhases + p] = s.prof[p];
+  s.prof_set(kTSaved, WaveHip::realtime());
+  WaveHip::sync();
+  if (prof_out != nullptr)
+    for (int p = WaveHip::lane(); p < kNumPhases; p += 64) prof_out[(int64_t)eid * kNumPhases + p] = s.prof[p];
 #else
   (void)prof_out;
 #endif

@@ -142,7 +142,7 @@ struct StateOffsets {
       sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/;
   int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
-      sc_row_of /*int16[S]*/;
+      sc_row_of /*int16[S]*/, sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build only*/;
 };
 
 constexpr int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
@@ -211,6 +211,10 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   s = align16(s + T);
   O.sc_row_of = s;
   s = align16(s + 2 * S);
+  O.sc_prof = s;
+#ifdef SSIM_PROFILE
+  s += 8 * 64;
+#endif
   O.scratch_bytes = s;
   return O;
 }
@@ -242,7 +246,9 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
   L->scratch_bytes = O->scratch_bytes;
   // LDS per wave: [hot copy (if resident) | scratch]
   const int64_t need = O->hot_bytes + O->scratch_bytes;
-  O->lds_resident = (need <= kLdsBudget || (need <= kLdsBudgetBig && B <= kBigLdsMaxEnvs)) ? 1 : 0;
+  O->lds_resident = (!(cfg.flags & SSIM_CFG_FORCE_HBM) && (need <= kLdsBudget || (need <= kLdsBudgetBig && B <= kBigLdsMaxEnvs)))
+                        ? 1 : 0;
+  L->lds_resident = O->lds_resident;
   O->lds_bytes = O->scratch_bytes + (O->lds_resident ? O->hot_bytes : 0);
 
   // obs arena: each field is [B][per-env]

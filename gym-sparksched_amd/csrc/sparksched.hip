@@ -137,11 +137,26 @@ static int hip_check(hipError_t e, const char* what) {
 }
 
 // A launch with more than 64 KB of dynamic LDS (layout.h kLdsBudgetBig) needs the kernel's opt-in attribute. It is
-// per-device state, so it is set before every such launch (idempotent; only small batches take this path).
+// per-device, per-function state: the raised limit is remembered per (device, kernel) so the attribute call is made
+// once, not before every step launch (a small cache; a miss or a race at worst repeats the idempotent call).
 static int lds_opt_in(const void* fn, int64_t lds) {
   if (lds <= kLdsBudget) return SSIM_OK;
-  return hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                   "engine kernel LDS attribute");
+  struct Entry {
+    int dev;
+    const void* fn;
+    int64_t lds;
+  };
+  static Entry cache[64];
+  static int n_cache = 0;
+  int dev = 0;
+  int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+  if (rc != SSIM_OK) return rc;
+  for (int i = 0; i < n_cache && i < 64; ++i)
+    if (cache[i].dev == dev && cache[i].fn == fn && cache[i].lds >= lds) return SSIM_OK;
+  rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                 "engine kernel LDS attribute");
+  if (rc == SSIM_OK && n_cache < 64) cache[n_cache++] = Entry{dev, fn, lds};
+  return rc;
 }
 
 extern "C" int ssim_layout_for(const ssim_config* cfg, ssim_layout* out) {
@@ -257,15 +272,16 @@ static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t n
   const RolloutFn fn = pick_rollout(h->params, (flags & SSIM_ROLLOUT_WARMUP) != 0);
   const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
   if (rc != SSIM_OK) return rc;
-  if (budget > 0) {
-    if (h->ticket_slot) flags |= kFlagTicketSlot;
-    h->ticket_slot ^= 1;
-  }
+  // the budget slot this launch claims from; flipped only once the launch is enqueued (a failed launch leaves the
+  // slot it would have zeroed dirty, so the next launch must use the same one again)
+  if (budget > 0 && h->ticket_slot) flags |= kFlagTicketSlot;
   hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64),
                      (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, flags, time_limits, h->reset, action_log,
                      (uint64_t*)nullptr, budget, env_steps);
-  return hip_check(hipGetLastError(), "k_rollout launch");
+  const int rc2 = hip_check(hipGetLastError(), "k_rollout launch");
+  if (rc2 == SSIM_OK && budget > 0) h->ticket_slot ^= 1;
+  return rc2;
 }
 
 extern "C" int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
@@ -308,7 +324,10 @@ extern "C" int ssim_reset_sampled(ssim_handle* h, const uint8_t* mode, const uin
 extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
                                      uint64_t* prof_out, void* stream) {
   const ssim_layout& L = h->params.L;
-  hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+  const RolloutFn fn = pick_rollout(h->params);
+  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  if (rc != SSIM_OK) return rc;
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, 0, (const double*)nullptr, h->reset,
                      (int32_t*)nullptr, prof_out, (int64_t)0, (const int32_t*)nullptr);
   return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
@@ -318,12 +337,17 @@ extern "C" int ssim_rollout_budget_profiled(ssim_handle* h, int32_t kind, uint64
                                             int64_t total_decisions, int32_t flags, uint64_t* prof_out,
                                             void* stream) {
   const ssim_layout& L = h->params.L;
+  if (total_decisions <= 0) return set_err(SSIM_E_ARG, "ssim_rollout_budget_profiled: total_decisions must be > 0");
+  const RolloutFn fn = pick_rollout(h->params);
+  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  if (rc != SSIM_OK) return rc;
   if (h->ticket_slot) flags |= kFlagTicketSlot;
-  h->ticket_slot ^= 1;
-  hipLaunchKernelGGL(pick_rollout(h->params), dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, max_steps, flags, (const double*)nullptr, h->reset,
                      (int32_t*)nullptr, prof_out, total_decisions, (const int32_t*)nullptr);
-  return hip_check(hipGetLastError(), "k_rollout(budget, profiled) launch");
+  const int rc2 = hip_check(hipGetLastError(), "k_rollout(budget, profiled) launch");
+  if (rc2 == SSIM_OK) h->ticket_slot ^= 1;
+  return rc2;
 }
 #endif
 

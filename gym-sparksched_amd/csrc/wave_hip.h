@@ -47,6 +47,11 @@ struct WaveHip {
     __builtin_amdgcn_wave_barrier();
   }
   __device__ static __forceinline__ uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+  __device__ static __forceinline__ uint64_t realtime() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
+  // no-return LDS atomic add (diagnostic profile build)
+  __device__ static __forceinline__ void lds_add_u64(uint64_t* p, uint64_t v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
   __device__ static __forceinline__ int excl_scan(int x, int* total) {
     int v = x;
     const int l = lane();

@@ -5,6 +5,7 @@ from __future__ import annotations
 import ctypes as ct
 
 SSIM_RESET_SKIP, SSIM_RESET_CONTINUE, SSIM_RESET_SEED = 0, 1, 2
+SSIM_CFG_FORCE_HBM = 1  # ssim_config.flags (test / diagnostic): hot blocks stay in HBM
 NUM_ACC = 8  # int64 accumulators per env (ob_acc): S_act, E_act, J_act, events, decisions, episodes, 0, 0
 ACC_NODES, ACC_EDGES, ACC_JOBS, ACC_EVENTS, ACC_DECISIONS, ACC_EPISODES = range(6)
 SSIM_ROLLOUT_AUTORESET = 0x1
@@ -48,7 +49,7 @@ class SsimConfig(ct.Structure):
         ("beta", ct.c_double),
         ("job_arrival_gap", ct.c_double),
         ("job_arrival_cap", ct.c_int32),
-        ("pad0", ct.c_int32),
+        ("flags", ct.c_int32),  # SSIM_CFG_*
     ]
 
 
@@ -97,7 +98,7 @@ class SsimResetRecord(ct.Structure):
 class SsimLayout(ct.Structure):
     _fields_ = [(n, ct.c_int32) for n in (
         "num_envs", "num_executors", "job_cap", "stage_cap", "edge_cap", "pool_cap", "set_cap", "commit_cap",
-        "trace_cap", "pad0")] + [(n, ct.c_int64) for n in (
+        "trace_cap", "lds_resident")] + [(n, ct.c_int64) for n in (
         "env_bytes", "state_bytes", "obs_bytes", "reset_bytes", "reset_stride", "scratch_bytes",
         "ob_nodes", "ob_edge_links", "ob_dag_ptr", "ob_supplies", "ob_frontier", "ob_sched_rank", "ob_counts",
         "ob_reward", "ob_wall_time", "ob_acc", "ob_trace")]

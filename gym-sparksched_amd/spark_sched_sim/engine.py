@@ -23,7 +23,8 @@ HEADER_RNG_OFFSET = 16  # EnvHeader: wall, time_limit, then the PCG64 words (lay
 PARAMS_RESERVE = 4096   # engine.h kParamsReserve
 
 
-def make_config(env_cfg: dict, num_envs: int, packed: PackedDataset, job_cap: int | None, trace_cap: int):
+def make_config(env_cfg: dict, num_envs: int, packed: PackedDataset, job_cap: int | None, trace_cap: int,
+                flags: int = 0):
     cap = job_cap if job_cap is not None else env_cfg.get("job_arrival_cap")
     if not cap:
         raise ValueError("job_cap is required when the env config has no job_arrival_cap")
@@ -39,6 +40,7 @@ def make_config(env_cfg: dict, num_envs: int, packed: PackedDataset, job_cap: in
         beta=float(env_cfg.get("beta", 0.0)),
         job_arrival_gap=(1 / env_cfg["job_arrival_rate"]) if env_cfg.get("job_arrival_rate") else 0.0,
         job_arrival_cap=int(env_cfg.get("job_arrival_cap") or 0),
+        flags=flags,
     )
 
 
@@ -185,7 +187,9 @@ class _ResetSampler:
 class DeviceEngine:
     """B independent envs on one GPU. All tensors live on `device`; nothing is copied per step."""
 
-    def __init__(self, env_cfg: dict, num_envs: int, dataset, device="cuda", job_cap=None, trace_cap: int = 0):
+    def __init__(self, env_cfg: dict, num_envs: int, dataset, device="cuda", job_cap=None, trace_cap: int = 0,
+                 config_flags: int = 0):
+        """config_flags: ssim_config.flags (SSIM_CFG_FORCE_HBM: hot blocks in HBM whatever their size, test use)."""
         import torch
 
         from . import native
@@ -196,7 +200,7 @@ class DeviceEngine:
         N = env_cfg["num_executors"]
         packed = dataset if isinstance(dataset, PackedDataset) else pack(dataset, N)
         self.packed = packed.with_executors(N)
-        self.cfg = make_config(env_cfg, num_envs, self.packed, job_cap, trace_cap)
+        self.cfg = make_config(env_cfg, num_envs, self.packed, job_cap, trace_cap, config_flags)
         self.num_envs = num_envs
         L = SsimLayout()
         native.check(native.lib().ssim_layout_for(ct.byref(self.cfg), ct.byref(L)), "ssim_layout_for")

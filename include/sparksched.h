@@ -58,8 +58,13 @@ typedef struct ssim_config {
   /* device-side job-sequence sampling (ssim_reset_sampled, rollout auto-reset; tpch.py:54-73) */
   double job_arrival_gap; /* 1 / job_arrival_rate, ms (computed by the caller, as Python does) */
   int32_t job_arrival_cap;/* 0 = no cap (time-limited episodes) */
-  int32_t pad0;
+  int32_t flags;          /* SSIM_CFG_* */
 } ssim_config;
+
+/* ssim_config.flags. SSIM_CFG_FORCE_HBM (test / diagnostic): keep every env's hot block in HBM (the kernels_hbm()
+ * instantiations) even when it would fit the LDS, so small batches exercise the HBM-resident path the large
+ * configurations run. */
+#define SSIM_CFG_FORCE_HBM 1
 
 /* Packed TPC-H-format dataset (device pointers). Built on the host from the raw per-query dicts by the
  * packer, which restates tpch.py:135-206 (preprocessing, num_tasks, rough duration). Template id =
@@ -103,7 +108,7 @@ typedef struct ssim_reset_record {
  * absolute within the obs arena, each field strided per env as documented. */
 typedef struct ssim_layout {
   int32_t num_envs, num_executors, job_cap, stage_cap, edge_cap, pool_cap, set_cap, commit_cap, trace_cap;
-  int32_t pad0;
+  int32_t lds_resident;    /* 1: the engine kernels hold each env's hot block in LDS for a launch, 0: in HBM */
   int64_t env_bytes, state_bytes, obs_bytes, reset_bytes, reset_stride, scratch_bytes;
   /* obs arena (zero-copy views):                                           element   per-env shape   */
   int64_t ob_nodes;        /* float32  [stage_cap][3]  (remaining, most_recent_duration, schedulable) */

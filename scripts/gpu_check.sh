@@ -19,15 +19,17 @@ for s in "$@"; do
   case "$s" in
     smoke)   step smoke 300 python __graft_entry__.py ;;
     pytest)  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    pytestall) step pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread ;;
     pytestk) step pytest_k 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PYTEST_K" ;;
     bench_driver) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     bench)   step bench 400 python bench.py ;;
     bench_nocpu) step bench_nocpu 300 python bench.py --no-cpu-baseline ;;
     bench_step) step bench_step 300 python bench.py --no-cpu-baseline --mode step ;;
     bench_decima) step bench_decima 400 python bench.py --workload decima --steps 40 --warmup 5 ;;
-    bench_ppo) step bench_ppo 900 python bench.py --workload ppo --steps 1 --warmup 0 --ppo-time-limit 2e6 ;;
+    bench_ppo) step bench_ppo 900 python bench.py --workload ppo --steps 1 --warmup 0 ;;
     prof_decima) step prof_decima 600 python scripts/profile_decima.py ;;
     bench_large) step bench_large 400 python bench.py --workload large --steps 100 --warmup 20 ;;
+    bench_cap850) step bench_cap850 300 python bench.py --no-cpu-baseline --dataset-seed 1 ;;
     prof)    step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     phase)   step phase 600 python scripts/phase_profile.py ;;
     sweep)   step sweep 900 bash scripts/steps_sweep.sh ;;

@@ -605,3 +605,123 @@ def case_async_rollouts(make, dataset, env_cfg, device="cpu", B=6, calls=3, dura
             total_resets += len(resets)
         parity.compare_obs(ob, obs_dict(v, e), f"env{e} final")
     assert total_resets >= B, total_resets
+
+
+def _env_trace(eng, i: int, n: int):
+    """Env i's trace records (the current episode), read without copying the whole obs arena to the host."""
+    raw = eng.views["trace"][i]
+    raw = raw.cpu().numpy() if hasattr(raw, "cpu") else np.asarray(raw)
+    return decode_trace(raw, n)
+
+
+def bench_time_limits(mean_limit, seeds):
+    """bench.py's per-env StochasticTimeLimit draws (seed 42 sampler, one draw per env with its reset seed)."""
+    from spark_sched_sim.wrappers import StochasticTimeLimitSampler
+
+    if not mean_limit:
+        return None
+    smp = StochasticTimeLimitSampler(mean_limit, len(seeds), seed=42)
+    return np.array([smp.sample(i, int(seeds[i])) for i in range(len(seeds))], dtype=np.float64)
+
+
+def replay_with_autoreset(cfg, dataset, seed, limit, actions, trace=False):
+    """The oracle driven through `actions` from reset(seed), restarting like the device's auto-reset: after a step
+    that terminates the episode or reaches its time limit, reset(seed=None) with the same limit. Returns the oracle,
+    its last observation, the episode count, the decisions of the current episode and the last step's reward (None
+    if the last step ended an episode)."""
+    limit = float("inf") if limit is None else float(limit)
+    o = SparkSchedOracle(cfg, dataset)
+    if trace:
+        o.trace = []
+    ob, _ = o.reset(seed=seed, options={"time_limit": limit})
+    ep, dec, last = 1, 0, None
+    for a in actions:
+        ob, rew, term, _, info = o.step({"stage_idx": int(a[0]), "num_exec": int(a[1])})
+        dec, last = dec + 1, rew
+        if term or info["wall_time"] >= limit:
+            if trace:
+                o.trace = []
+            ob, _ = o.reset(seed=None, options={"time_limit": limit})
+            ep, dec, last = ep + 1, 0, None
+    return o, ob, ep, dec, last
+
+
+def check_replayed_env(eng, v, ta, tc, i, o, ob, ep, dec, last, what, trace=False):
+    c = v["counts"][i]
+    assert int(c[_abi.OC_ERR]) == 0, f"{what} env{i} err {int(c[_abi.OC_ERR])}"
+    assert int(c[_abi.OC_EPISODE]) == ep, f"{what} env{i} episodes {int(c[_abi.OC_EPISODE])} != {ep}"
+    assert int(c[_abi.OC_DECISIONS]) == dec, f"{what} env{i} decisions {int(c[_abi.OC_DECISIONS])} != {dec}"
+    assert float(v["wall_time"][i]) == float(o.wall_time), f"{what} env{i} wall time"
+    if last is not None:
+        assert float(v["reward"][i]) == pytest.approx(float(last), rel=1e-9, abs=1e-12), f"{what} env{i} reward"
+    parity.compare_obs(ob, obs_dict(v, i), f"{what} env{i} final")
+    for jid, job in o.jobs.items():
+        assert ta[i][jid] == job.t_arrival, f"{what} env{i} job {jid} arrival"
+        assert tc[i][jid] == job.t_completed or (np.isinf(tc[i][jid]) and np.isinf(job.t_completed)), \
+            f"{what} env{i} job {jid} completion"
+    if trace:
+        n = int(c[_abi.OC_TRACE_LEN])
+        ref = [tuple(float(x) if j == 0 else int(x) for j, x in enumerate(r)) for r in o.trace]
+        assert len(ref) == n and _env_trace(eng, i, n) == ref, f"{what} env{i} trace"
+
+
+def case_bench_rollout_sequence(make, dataset, cfg, B, preroll, warmup, K, stride, mean_limit=None, trace_cap=0,
+                                seed=0, rank=0, expect_resident=None):
+    """bench.py's rollout sequence verbatim (bench.py main(), rollout mode): the device reset with the rank's shard
+    seeds and StochasticTimeLimit draws; the seeded pre-roll of U[0, preroll) decisions per env (ssim_rollout_steps,
+    AUTORESET | WARMUP); one warm-up launch of `warmup` steps and the timed launch of K steps, both shared-budget
+    launches of B x steps decisions at most 8 x steps per env (ssim_rollout_budget, PREEMPT | AUTORESET); then a
+    closing launch of 0 steps, which completes the steps the timed launch preempted. Every launch logs its
+    actions; each sampled env's actions, concatenated in launch order and replayed on the oracle with the same
+    auto-resets (terminated, or truncated by the time limit), give its episode count, the decisions, wall time,
+    job arrival / completion times and final observation of its current episode bit for bit (and, with trace_cap,
+    that episode's event trace). Reference: spark_sched_sim.py:127-343 (reset, step, the event loop)."""
+    from spark_sched_sim.distributed import shard_seeds
+
+    SENT = -99
+    AR, PRE, WU = _abi.SSIM_ROLLOUT_AUTORESET, _abi.SSIM_ROLLOUT_PREEMPT, _abi.SSIM_ROLLOUT_WARMUP
+    kind = _abi.SSIM_POLICY_RANDOM
+    eng = make(cfg, B, dataset, trace_cap)
+    if expect_resident is not None:
+        assert int(eng.layout.lds_resident) == int(expect_resident), "kernel path (LDS / HBM residency)"
+    seeds = shard_seeds(rank, B, seed)
+    lim = bench_time_limits(mean_limit, seeds)
+    eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=lim)
+    actions = [[] for _ in range(B)]
+
+    def collect(log):
+        lg = np.asarray(eng.to_numpy(log))
+        n = 0
+        for i in range(B):
+            rows = lg[:, i, 0] != SENT
+            actions[i].extend(lg[rows, i].tolist())
+            n += int(rows.sum())
+        return n
+
+    pre = np.random.default_rng([seed, rank, 7]).integers(0, preroll, B).astype(np.int32)
+    log = eng.alloc_action_log(int(pre.max()) + 1)
+    log.fill_(SENT)
+    eng.rollout_steps(kind, 4321, pre, int(pre.max()) + 1, log, flags=AR | WU, time_limits=lim)
+    assert collect(log) == int(pre.sum())
+    acc0 = np.array(eng.to_numpy(eng.views["acc"]), dtype=np.int64).copy()
+    for c, f in ((warmup, AR | PRE | WU), (K, AR | PRE)):
+        log = eng.alloc_action_log(8 * c)
+        log.fill_(SENT)
+        eng.rollout_budget(kind, 1234, 8 * c, B * c, log, flags=f, time_limits=lim)
+        assert collect(log) == B * c  # every launch hands out exactly its budget
+    pend = np.asarray(eng.to_numpy(eng.views["counts"]))[:, _abi.OC_ERR] & _abi.SSIM_ERR_PENDING
+    eng.rollout(kind, 1234, 0, flags=AR, time_limits=lim)  # closing launch: completes the pending steps
+    v = eng.host_views()
+    ta, tc, _ = eng.job_times_np()
+    applied = np.array([len(a) for a in actions])
+    d_acc = (np.asarray(v["acc"], dtype=np.int64) - acc0).sum(axis=0)
+    assert int(d_acc[_abi.ACC_DECISIONS]) == B * (warmup + K)  # every claimed decision completed, none twice
+    assert int(np.count_nonzero(v["counts"][:, _abi.OC_ERR])) == 0
+    episodes = 0
+    for i in range(0, B, stride):
+        o, ob, ep, dec, last = replay_with_autoreset(cfg, dataset, seeds[i], None if lim is None else lim[i],
+                                                     actions[i], trace=trace_cap > 0)
+        check_replayed_env(eng, v, ta, tc, i, o, ob, ep, dec, last, "bench-sequence", trace=trace_cap > 0)
+        episodes += ep
+    return {"pending_at_timed_end": int(np.count_nonzero(pend)), "episodes_replayed": episodes,
+            "decisions_replayed": int(applied[::stride].sum()), "episodes_total": int(v["counts"][:, _abi.OC_EPISODE].sum())}

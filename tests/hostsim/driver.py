@@ -19,7 +19,9 @@ from spark_sched_sim._abi import SsimConfig, SsimDataset, SsimLayout  # noqa: E4
 from spark_sched_sim.data_samplers.tpch_pack import PackedDataset, pack  # noqa: E402
 from spark_sched_sim.engine import _ResetSampler, arena_views, make_config  # noqa: E402
 
-SO_PATH = os.path.join(HERE, "_hostsim.so")
+# HOSTSIM_SO / HOSTSIM_FLAGS: a variant build (e.g. scripts/hostsim_sanitize.sh: -DSSIM_PROFILE under ASan/UBSan)
+SO_PATH = os.environ.get("HOSTSIM_SO") or os.path.join(HERE, "_hostsim.so")
+ENV_FLAGS = os.environ.get("HOSTSIM_FLAGS", "").split()
 SOURCES = [os.path.join(HERE, "hostsim.cpp")] + [
     os.path.join(REPO, "gym-sparksched_amd", "csrc", f) for f in ("engine.h", "policy.h", "pyset.h", "pcg64.h", "decima.h", "fdlibm.h", "ziggurat.h",
                                                                   "layout.h")] + [
@@ -45,7 +47,7 @@ def build(force: bool = False, extra_flags=()) -> str:
             tmp = f"{SO_PATH}.{os.getpid()}.tmp"
             cmd = ["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
                    "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}",
-                   f"-I{os.path.join(REPO, 'gym-sparksched_amd', 'csrc')}", SOURCES[0], "-o", tmp, *extra_flags]
+                   f"-I{os.path.join(REPO, 'gym-sparksched_amd', 'csrc')}", SOURCES[0], "-o", tmp, *extra_flags, *ENV_FLAGS]
             subprocess.run(cmd, check=True)
             os.replace(tmp, SO_PATH)
     return SO_PATH

@@ -39,6 +39,8 @@ struct WaveSerial {
   static void sync() {}
   static void gsync() {}
   static uint64_t clock() { return 0; }
+  static uint64_t realtime() { return 0; }
+  static void lds_add_u64(uint64_t* p, uint64_t v) { *p += v; }
   static int excl_scan(int x, int* total) {
     *total = x;
     return 0;

@@ -320,11 +320,11 @@ def test_cat_batches_equals_select_of_all(dataset):
 @pytest.mark.gpu
 def test_ppo_decima_tpch_iteration_gpu(gpu_device, dataset):
     """BASELINE configs[4] on the device: one PPO iteration of config/decima_tpch.yaml (4 sequences x 4 rollouts,
-    N=50, J cap 200, beta 5e-3, the Decima architecture through the fused policy kernel; mean time limit shortened
-    to 1e6 ms so the oracle replay stays short). Checks:
+    N=50, J cap 200, beta 5e-3, the Decima architecture through the fused policy kernel) at the yaml's
+    mean_time_limit 2e7 ms (config/decima_tpch.yaml:87, applied at rollout_worker.py:83). Checks:
       * returns and baselines of the gathered batch equal the numpy restatement of returns_calculator.py /
         baselines.py (oracle/trainer_utils.py) within 1e-12 relative;
-      * every other row's logged actions replayed on the oracle (StochasticTimeLimit seeded as the trainer does)
+      * every 4th row's logged actions replayed on the oracle (StochasticTimeLimit seeded as the trainer does)
         reproduce its wall times bit for bit, its rewards within 1e-9 and its episode length exactly;
       * the learner's update runs (finite losses) and changes the parameters."""
     from oracle.restatement import SparkSchedOracle
@@ -332,7 +332,8 @@ def test_ppo_decima_tpch_iteration_gpu(gpu_device, dataset):
     from spark_sched_sim.trainers import DECIMA_TPCH, PPO
 
     cfg = {k: dict(v) for k, v in DECIMA_TPCH.items()}
-    cfg["env"]["mean_time_limit"] = 1.0e6
+    mean_limit = cfg["env"]["mean_time_limit"]
+    assert mean_limit == 2.0e7
     ppo = PPO(cfg["agent"], cfg["env"], cfg["trainer"], dataset=dataset, device=gpu_device)
     assert ppo.collector.fused
     seeds = ppo._seeds()
@@ -353,8 +354,9 @@ def test_ppo_decima_tpch_iteration_gpu(gpu_device, dataset):
     si, ei = acts["stage_idx"].cpu().numpy(), acts["exec_idx"].cpu().numpy()
     off = np.concatenate([[0], np.cumsum(n)])
     env_cfg = {k: v for k, v in ppo.env_cfg.items() if k not in ("mean_time_limit", "dataset")}
-    for i in range(0, R, 2):
-        limit = float(np.random.RandomState(seeds[i]).exponential(1.0e6))
+    assert int(lengths.max()) > 500  # long episodes: the J=200 capacity is exercised
+    for i in range(0, R, 4):
+        limit = float(np.random.RandomState(seeds[i]).exponential(mean_limit))
         o = SparkSchedOracle(env_cfg, dataset)
         o.reset(seed=seeds[i], options={"time_limit": limit})
         for k in range(n[i]):
