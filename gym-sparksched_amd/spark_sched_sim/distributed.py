@@ -56,6 +56,32 @@ def split_rows(total: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def gather_var(t, world: int, rank: int, dst: int = 0):
+    """gather to rank `dst` of tensors whose first dimension differs across ranks (sizes all-gathered, payload
+    padded to the max and gathered to `dst` only). Returns the per-rank tensors in rank order on `dst`, None
+    elsewhere. bool tensors travel as uint8."""
+    if world <= 1:
+        return [t]
+    import torch
+    import torch.distributed as dist
+
+    is_bool = t.dtype == torch.bool
+    x = t.to(torch.uint8) if is_bool else t
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    sizes = [int(v.item()) for v in ns]
+    m = max(sizes)
+    pad = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    pad[: x.shape[0]] = x
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad.contiguous(), parts, dst=dst)
+    if rank != dst:
+        return None
+    out = [p[:k] for p, k in zip(parts, sizes)]
+    return [o.bool() for o in out] if is_bool else out
+
+
 def all_gather_var(t, world: int) -> list:
     """all_gather of tensors whose first dimension differs across ranks (padded to the max, then trimmed).
     Returns the per-rank tensors in rank order. bool tensors travel as uint8 (gloo has no bool)."""

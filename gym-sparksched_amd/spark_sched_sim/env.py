@@ -66,6 +66,10 @@ def _raise_for(err: int, action) -> None:
         raise AssertionError("simulator invariant violated (reference `assert`)")
     if err & (_abi.SSIM_ERR_CAPACITY | _abi.SSIM_ERR_RESET):
         raise RuntimeError(f"device capacity/reset error {err:#x}")
+    if err & _abi.SSIM_ERR_PENDING:
+        # a step preempted by a budget launch (SSIM_ROLLOUT_PREEMPT) was completed instead: this action, chosen on
+        # the observation before that step, was NOT applied
+        raise RuntimeError("a preempted step was completed by this call; the action was not applied")
 
 
 class SparkSchedSimEnv(_EnvBase):

@@ -36,7 +36,9 @@ class RowStats:
                         (one deque(maxlen=200), spark_sched_sim.py:83,243-245,697), in seconds;
       avg_num_jobs      metrics.avg_num_jobs of the current episode (durations of active and completed jobs up
                         to the wall time, / wall time);
-      num_completed_jobs, num_job_arrivals (completed + active) of the current episode.
+      num_completed_jobs, num_job_arrivals of the current episode: the reference's num_job_arrivals is
+                        num_completed_jobs + num_active_jobs (rollout_worker.py:126-127), i.e. the arrived jobs
+                        (state 1 or 2 here) -- not the completed count.
     Call `flush(rows, engine)` before an engine resets `rows` (their finished episode's completions enter the
     windows); `stats(engine)` -> float64 [B, 4]. Completions enter a window in completion-time order (stable in
     job id for equal times)."""

@@ -27,7 +27,7 @@ from typing import Any
 import numpy as np
 import torch
 
-from ..distributed import all_gather_var, split_rows
+from ..distributed import all_gather_var, gather_var, split_rows
 from ..schedulers.decima import DagBatch, DecimaScheduler, cat_batches, select_envs
 from .returns import Baseline, ReturnsCalculator
 from .rollouts import AsyncRolloutCollector, RolloutCollector
@@ -43,22 +43,27 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() else None
 
 
-def gather_batches(b: DagBatch, world: int) -> DagBatch:
-    """Every rank's DagBatch concatenated in rank order (all_gather of each field, then cat_batches)."""
+def gather_batches(b: DagBatch, world: int, rank: int = 0, dst: int = 0) -> DagBatch | None:
+    """Every rank's DagBatch concatenated in rank order on rank `dst` (a gather of each field, then cat_batches);
+    None on the other ranks, which do not train (the single learner of trainer.py:126-131)."""
     if world <= 1:
         return b
     parts = {}
     for name in _BATCH_TENSORS:
         t = getattr(b, name)
         if name == "edge_index":
-            parts[name] = [p.t() for p in all_gather_var(t.t().contiguous(), world)]
+            g = gather_var(t.t().contiguous(), world, rank, dst)
+            parts[name] = None if g is None else [p.t() for p in g]
         elif name in ("ptr", "obs_ptr"):  # drop the leading 0 for the variable gather, restore per rank
-            parts[name] = [torch.cat([torch.zeros(1, dtype=p.dtype, device=p.device), p])
-                           for p in all_gather_var(t[1:].contiguous(), world)]
+            g = gather_var(t[1:].contiguous(), world, rank, dst)
+            parts[name] = None if g is None else [torch.cat([torch.zeros(1, dtype=p.dtype, device=p.device), p])
+                                                  for p in g]
         else:
-            parts[name] = all_gather_var(t, world)
+            parts[name] = gather_var(t, world, rank, dst)
     scal = torch.tensor([b.max_levels, b.num_envs, b.max_nodes], dtype=torch.int64, device=b.x.device)
-    scals = all_gather_var(scal[None, :], world)
+    scals = gather_var(scal[None, :], world, rank, dst)
+    if rank != dst:
+        return None
     bs = []
     for k in range(world):
         ml, ne, mn = (int(v) for v in scals[k][0].tolist())
@@ -159,7 +164,9 @@ class PPO:
     # ------------------------------------------------------------------ learning
     def gather_rollouts(self, buf):
         """This rank's buffer in row-major (row, decision) order, gathered over all ranks to one batch in global
-        row order: (times [R, T+1], rewards [R, T], lengths [R], obs DagBatch, actions) on every rank."""
+        row order: (times [R, T+1], rewards [R, T], lengths [R], obs DagBatch, actions). times / rewards / lengths
+        are all-gathered (every rank keeps the differential-return window in step); the observations and actions
+        go to the learner (rank 0) only, None elsewhere."""
         times, rewards, lengths, sample = buf.trajectories()
         obs, acts = buf.samples()
         canon = sample[sample >= 0]  # row-major: row r's decisions in order, rows ascending
@@ -177,8 +184,9 @@ class PPO:
             times = torch.cat(all_gather_var(times, self.world))
             rewards = torch.cat(all_gather_var(rewards, self.world))
             lengths = torch.cat(all_gather_var(lengths, self.world))
-            obs = gather_batches(obs, self.world)
-            acts = {k: torch.cat(all_gather_var(v, self.world)) for k, v in acts.items()}
+            obs = gather_batches(obs, self.world, self.rank, 0)
+            g = {k: gather_var(v, self.world, self.rank, 0) for k, v in acts.items()}
+            acts = None if self.rank != 0 else {k: torch.cat(v) for k, v in g.items()}
         return times, rewards, lengths, obs, acts
 
     def train_on_rollouts(self, buf) -> dict[str, Any]:

@@ -115,7 +115,11 @@ class SparkSchedSimVecEnv:
 
     def _info(self):
         c = self.engine.views["counts"]
-        return {"wall_time": self.engine.views["wall_time"], "err": c[:, _abi.OC_ERR],
+        err = c[:, _abi.OC_ERR]
+        # action_dropped: envs whose step call completed a step a budget launch had preempted
+        # (SSIM_ROLLOUT_PREEMPT) instead of applying the given action (SSIM_ERR_PENDING)
+        return {"wall_time": self.engine.views["wall_time"], "err": err,
+                "action_dropped": (err & _abi.SSIM_ERR_PENDING) != 0,
                 "decisions": c[:, _abi.OC_DECISIONS], "num_completed_jobs": c[:, _abi.OC_NUM_COMPLETED]}
 
     def episode_stats(self):

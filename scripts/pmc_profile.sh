@@ -5,8 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 MODE=${PMC_MODE:-rollout}
 # default: the driver's bench command (bench.py --steps 20 --warmup 5)
-if [ "$MODE" = rollout ]; then ARGS=${PMC_ARGS:-"--steps 20 --warmup 5"}; else ARGS="--steps 100 --warmup 20"; fi
-OUT=gpurun_out/pmc_$MODE
+if [ "$MODE" = rollout ]; then ARGS=${PMC_ARGS:-"--steps 20 --warmup 5"}; else ARGS=${PMC_ARGS:-"--steps 100 --warmup 20"}; fi
+OUT=gpurun_out/pmc_${PMC_TAG:-$MODE}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 run() {

@@ -704,18 +704,23 @@ def case_bench_rollout_sequence(make, dataset, cfg, B, preroll, warmup, K, strid
     eng.rollout_steps(kind, 4321, pre, int(pre.max()) + 1, log, flags=AR | WU, time_limits=lim)
     assert collect(log) == int(pre.sum())
     acc0 = np.array(eng.to_numpy(eng.views["acc"]), dtype=np.int64).copy()
+    started = 0
     for c, f in ((warmup, AR | PRE | WU), (K, AR | PRE)):
         log = eng.alloc_action_log(8 * c)
         log.fill_(SENT)
         eng.rollout_budget(kind, 1234, 8 * c, B * c, log, flags=f, time_limits=lim)
-        assert collect(log) == B * c  # every launch hands out exactly its budget
+        n = collect(log)
+        # the launch hands out its budget in chunks of <= 8 decisions; a wave stopped by preemption (or its step cap)
+        # while holding part of a chunk leaves that part unstarted, so the steps started are within 8 per env of it
+        assert B * c - 8 * B <= n <= B * c, (n, B * c)
+        started += n
     pend = np.asarray(eng.to_numpy(eng.views["counts"]))[:, _abi.OC_ERR] & _abi.SSIM_ERR_PENDING
     eng.rollout(kind, 1234, 0, flags=AR, time_limits=lim)  # closing launch: completes the pending steps
     v = eng.host_views()
     ta, tc, _ = eng.job_times_np()
     applied = np.array([len(a) for a in actions])
     d_acc = (np.asarray(v["acc"], dtype=np.int64) - acc0).sum(axis=0)
-    assert int(d_acc[_abi.ACC_DECISIONS]) == B * (warmup + K)  # every claimed decision completed, none twice
+    assert int(d_acc[_abi.ACC_DECISIONS]) == started  # every started decision completed, none twice
     assert int(np.count_nonzero(v["counts"][:, _abi.OC_ERR])) == 0
     episodes = 0
     for i in range(0, B, stride):
