@@ -233,6 +233,24 @@ struct Sim {
   EnvHeader h;    // register copy of the header
   Pcg64 rng;
   uint32_t iv_lane;  // Params::iv row `lane` (device: read with v_readlane instead of a scalar-cache load)
+  // Executor event slots in registers (device waves): lane l of page p holds executor 64p + l's pending event, a
+  // write-through copy of the ExecRec fields ev_t / ev_seq / ev_type / ev_stage (the hot block stays authoritative
+  // for lane-parallel readers and across launches). The event pop then reads no memory: a DPP min over registers
+  // instead of a reload of every executor record per event (an LDS round trip on the resident kernels, HBM lines on
+  // the HBM-resident ones). Pages: the executor count's when it is a compile-time constant, else
+  // SSIM_EV_PAGES_GENERIC (per translation unit: 2 = up to 128 executors in k_hbm.hip, 1 in k_lds.hip, where two
+  // pages crash the ROCm 7.2 register allocator); more executors fall back to the record reads.
+#ifndef SSIM_EV_PAGES_GENERIC
+#define SSIM_EV_PAGES_GENERIC 1
+#endif
+  static constexpr int kEvPages = W::kWidth == 64 ? (kN > 0 ? (kN + 63) / 64 : SSIM_EV_PAGES_GENERIC) : 0;
+  struct EvRegs {
+    uint32_t tlo, thi;  // ev_t bits (+inf: no event)
+    int32_t seq;        // -1: no event
+    int32_t ts;         // ev_type << 16 | (uint16) ev_stage
+  };
+  EvRegs evr[kEvPages > 0 ? kEvPages : 1];
+  __device__ __forceinline__ bool ev_in_regs() const { return kEvPages > 0 && NE <= 64 * kEvPages; }
   const HotParams* HPp;  // host build: Params::hp read in place
   uint32_t hpv;          // device: dword `lane` of Params::hp
 #ifdef SSIM_PROFILE
@@ -296,6 +314,9 @@ struct Sim {
   // initialised at arrival (on_job_arrival), so nothing outside the range is read during the launch.
   // A copy issues up to kCopyBatch 16-B loads per lane before any store (one memory latency per batch).
   static constexpr int kCopyBatch = 12;
+  // 16 bytes as a native vector (one dwordx4 load / store). HIP's uint4 is a struct with a union inside, and the
+  // copy's array of them was placed in scratch memory (a store and a reload per element through the scratch path).
+  typedef uint32_t u32x4 __attribute__((vector_size(16)));
   struct Span {
     int64_t off, n;  // byte offset in the hot block, 16-B units
   };
@@ -307,7 +328,7 @@ struct Sim {
 #pragma unroll
     for (int r = 0; r < kSpans; ++r) end[r] = (total += sp[r].n);
     for (int64_t i0 = 0; i0 < total; i0 += (int64_t)W::kWidth * kCopyBatch) {
-      uint4 v[kCopyBatch];
+      u32x4 v[kCopyBatch];
       int64_t at[kCopyBatch];
 #pragma unroll
       for (int u = 0; u < kCopyBatch; ++u) {
@@ -317,11 +338,11 @@ struct Sim {
         for (int r = kSpans - 1; r >= 0; --r)
           if (i < end[r]) o = sp[r].off + (i - (end[r] - sp[r].n)) * 16;  // (a later r overwrites: may be < 0)
         at[u] = i < total ? o : -1;
-        if (at[u] >= 0) v[u] = *reinterpret_cast<const uint4*>(src + at[u]);
+        if (at[u] >= 0) v[u] = *reinterpret_cast<const u32x4*>(src + at[u]);
       }
 #pragma unroll
       for (int u = 0; u < kCopyBatch; ++u)
-        if (at[u] >= 0) *reinterpret_cast<uint4*>(dst + at[u]) = v[u];
+        if (at[u] >= 0) *reinterpret_cast<u32x4*>(dst + at[u]) = v[u];
     }
     W::sync();
   }
@@ -385,6 +406,7 @@ struct Sim {
                             list_span(O.sched_list, h.n_sched)};
       copy_spans(hot, ghot, live);
     }
+    ev_regs_load();
     SSIM_TOC(t0, kPhLoadSave);
   }
   // Requires the header stored (store_header) and in registers (the state after a step or a preemption).
@@ -1014,12 +1036,62 @@ struct Sim {
   }
 
   // ---------------------------------------------------------------- events (event.py)
+  // Register event slots (evr): (re)loaded from the executor records after the hot block is in place, and updated
+  // together with the records by every writer of an event field (push_event, run_next_task_rec, pop_event, reset).
+  __device__ __forceinline__ void ev_regs_load() {
+    if constexpr (kEvPages > 0) {
+#pragma unroll
+      for (int p = 0; p < kEvPages; ++p) {
+        const int e = 64 * p + W::lane();
+        ExecRec r{};
+        r.ev_seq = -1;
+        r.ev_t = __builtin_inf();
+        if (e < NE) r = exr(e);
+        const uint64_t b = __builtin_bit_cast(uint64_t, r.ev_seq >= 0 ? r.ev_t : __builtin_inf());
+        evr[p].tlo = (uint32_t)b;
+        evr[p].thi = (uint32_t)(b >> 32);
+        evr[p].seq = r.ev_seq >= 0 ? r.ev_seq : -1;
+        evr[p].ts = ((int32_t)r.ev_type << 16) | (uint16_t)r.ev_stage;
+      }
+    }
+  }
+  __device__ __forceinline__ void ev_regs_set(int e, double t, int seq, int type, int g) {
+    if constexpr (kEvPages > 0) {
+      const uint64_t b = __builtin_bit_cast(uint64_t, t);
+      const int l = e & 63, pg = e >> 6;
+#pragma unroll
+      for (int p = 0; p < kEvPages; ++p) {
+        if (p == pg) {  // (uniform)
+          evr[p].tlo = (uint32_t)W::writelane((int)(uint32_t)b, l, (int)evr[p].tlo);
+          evr[p].thi = (uint32_t)W::writelane((int)(uint32_t)(b >> 32), l, (int)evr[p].thi);
+          evr[p].seq = W::writelane(seq, l, evr[p].seq);
+          evr[p].ts = W::writelane((type << 16) | (g & 0xFFFF), l, evr[p].ts);
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void ev_regs_clear(int e) {
+    if constexpr (kEvPages > 0) {
+      const uint64_t b = __builtin_bit_cast(uint64_t, (double)__builtin_inf());
+      const int l = e & 63, pg = e >> 6;
+#pragma unroll
+      for (int p = 0; p < kEvPages; ++p) {
+        if (p == pg) {
+          evr[p].tlo = (uint32_t)W::writelane((int)(uint32_t)b, l, (int)evr[p].tlo);
+          evr[p].thi = (uint32_t)W::writelane((int)(uint32_t)(b >> 32), l, (int)evr[p].thi);
+          evr[p].seq = W::writelane(-1, l, evr[p].seq);
+        }
+      }
+    }
+  }
   __device__ __forceinline__ void push_event(int e, double t, int type, int g) {
     check(ev_seq(e) < 0);  // at most one pending event per executor (DESIGN.md §Event queue)
+    const int sq = h.seq++;
     ev_t(e) = t;
-    ev_seq(e) = h.seq++;
+    ev_seq(e) = sq;
     ev_type(e) = (int16_t)type;
     ev_stage(e) = (int16_t)g;
+    ev_regs_set(e, t, sq, type, g);
   }
 
   __device__ __forceinline__ void trace(double t, int kind, int e, int job, int sid, int seq) {
@@ -1225,10 +1297,10 @@ struct Sim {
 
   // _execute_next_task (:584-615) on register copies of the stage and executor records (ld_rec), which the
   // caller writes back: the task-completion path then costs one LDS access per record, not one per field.
-  __device__ __forceinline__ void run_next_task_rec(int g, StageRec& s, ExecRec& x) {
-    run_next_task_rec(g, s, x, dur_gather(s.ts));
+  __device__ __forceinline__ void run_next_task_rec(int e, int g, StageRec& s, ExecRec& x) {
+    run_next_task_rec(e, g, s, x, dur_gather(s.ts));
   }
-  __device__ __forceinline__ void run_next_task_rec(int g, StageRec& s, ExecRec& x, const DurDesc& dd) {
+  __device__ __forceinline__ void run_next_task_rec(int e, int g, StageRec& s, ExecRec& x, const DurDesc& dd) {
     const int j = s.job;
     check(s.rem > 0);
     check(x.job == j);
@@ -1252,13 +1324,14 @@ struct Sim {
     x.ev_seq = h.seq++;
     x.ev_type = (int16_t)kEvTask;
     x.ev_stage = (int16_t)g;
+    ev_regs_set(e, x.ev_t, x.ev_seq, kEvTask, g);
   }
   __device__ __forceinline__ void run_next_task(int e, int g) {  // :584-615
     const StageRec sraw = stage(g);  // both records in one LDS round trip
     const ExecRec xraw = exr(e);
     StageRec s = ld_rec(sraw);
     ExecRec x = ld_rec(xraw);
-    run_next_task_rec(g, s, x);
+    run_next_task_rec(e, g, s, x);
     stage(g) = s;
     exr(e) = x;
   }
@@ -1482,7 +1555,7 @@ struct Sim {
     s.exe = (int16_t)(s.exe - 1);
     x.busy = 0;
     if (s.rem > 0) {  // the common case: the executor takes the stage's next task
-      run_next_task_rec(g, s, x, dd);
+      run_next_task_rec(e, g, s, x, dd);
       stage(g) = s;
       exr(e) = x;
       SSIM_MARK("task_done_fast_end");
@@ -1514,7 +1587,31 @@ struct Sim {
     // flight together with the executor records' instead of being waited on first (+1%; also fetching the job
     // record with the stage's and executor's, its id taken from the pop, measured -0.5%: profiles/r02/ab_lds_overlap.log)
     const double ta_lane = have_arr ? jtimes(h.arrivals).tarr : 0.0;
-    for (int k0 = 0; k0 < NE; k0 += kSpan) {
+    bool scanned = false;
+    if constexpr (kEvPages > 0) {
+      if (ev_in_regs()) {  // the register event slots: no memory read
+        scanned = true;
+#pragma unroll
+        for (int p = 0; p < kEvPages; ++p) {
+          if (64 * p >= NE) break;
+          const EvRegs r = evr[p];
+          const double tv = __builtin_bit_cast(double, ((uint64_t)r.thi << 32) | r.tlo);
+          double tt;
+          const int l = W::template argmin_event<kSpan>(tv, r.seq, r.seq >= 0, &tt);
+          if (l < 0) continue;
+          const int ss = W::bcast_i(r.seq, l);
+          if (be < 0 || tt < bt || (tt == bt && ss < bseq)) {
+            bt = tt;
+            bseq = ss;
+            be = 64 * p + l;
+            const int ts = W::bcast_i(r.ts, l);
+            btype = ts >> 16;
+            bstage = (int16_t)(ts & 0xFFFF);
+          }
+        }
+      }
+    }
+    for (int k0 = 0; !scanned && k0 < NE; k0 += kSpan) {
       const int k = k0 + W::lane();
       ExecRec r{};
       r.ev_seq = -1;
@@ -1551,6 +1648,7 @@ struct Sim {
     *g = bstage;
     *seq = bseq;
     ev_seq(be) = -1;
+    ev_regs_clear(be);
     return true;
   }
 
@@ -2134,6 +2232,7 @@ struct Sim {
       if (k < commit_cap_for(NE)) cm(k) = CommitRec{};
     }
     W::sync();
+    ev_regs_load();
     {
       uint8_t* t = S<uint8_t>(O.sc_tab_p);
       ps_init(pmeta(kPoolCommon), t);

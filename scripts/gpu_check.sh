@@ -47,8 +47,6 @@ for s in "$@"; do
     pmc300)  step pmc300 900 env PMC_TAG=k300 PMC_ARGS="--steps 300 --warmup 50" bash scripts/pmc_profile.sh ;;
     pmc_large) step pmc_large 900 env PMC_TAG=large PMC_ARGS="--workload large --steps 100 --warmup 20" bash scripts/pmc_profile.sh ;;
     pmc_decima) step pmc_decima 900 env PMC_TAG=decima PMC_ARGS="--workload decima --steps 40 --warmup 5" bash scripts/pmc_profile.sh ;;
-    pcs20)   step pcs20 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method "${PCS_METHOD:-stochastic}" --pc-sampling-unit "${PCS_UNIT:-cycles}" --pc-sampling-interval "${PCS_INTERVAL:-65536}" -d "$PWD/$OUT/pcs20" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 ;;
-    pcs)     step pcs 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method "${PCS_METHOD:-stochastic}" --pc-sampling-unit "${PCS_UNIT:-cycles}" --pc-sampling-interval "${PCS_INTERVAL:-65536}" -d "$PWD/$OUT/pcs" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 300 --warmup 5 ;;
     ab20x)   step ab20x 1200 env AB_TAG=s20 AB_ARGS="--steps 20 --warmup 5" AB_REPS=3 bash scripts/ab_tpch.sh ;;
     prof_step) step prof_step 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_step" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -722,11 +722,16 @@ def case_bench_rollout_sequence(make, dataset, cfg, B, preroll, warmup, K, strid
     d_acc = (np.asarray(v["acc"], dtype=np.int64) - acc0).sum(axis=0)
     assert int(d_acc[_abi.ACC_DECISIONS]) == started  # every started decision completed, none twice
     assert int(np.count_nonzero(v["counts"][:, _abi.OC_ERR])) == 0
-    episodes = 0
-    for i in range(0, B, stride):
+    episodes, crossed = 0, 0
+    # every stride-th env, plus the first envs (up to 4 more) that went through an auto-reset
+    multi = [int(i) for i in np.nonzero(v["counts"][:, _abi.OC_EPISODE] > 1)[0] if i % stride][:4]
+    sample = sorted(set(range(0, B, stride)) | set(multi))
+    for i in sample:
         o, ob, ep, dec, last = replay_with_autoreset(cfg, dataset, seeds[i], None if lim is None else lim[i],
                                                      actions[i], trace=trace_cap > 0)
         check_replayed_env(eng, v, ta, tc, i, o, ob, ep, dec, last, "bench-sequence", trace=trace_cap > 0)
         episodes += ep
+        crossed += ep > 1
     return {"pending_at_timed_end": int(np.count_nonzero(pend)), "episodes_replayed": episodes,
-            "decisions_replayed": int(applied[::stride].sum()), "episodes_total": int(v["counts"][:, _abi.OC_EPISODE].sum())}
+            "crossed_replayed": crossed, "decisions_replayed": int(applied[sample].sum()),
+            "episodes_total": int(v["counts"][:, _abi.OC_EPISODE].sum())}

@@ -12,9 +12,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-struct uint4 {  // HIP vector type used by the (device-only) LDS residency copy; never taken on the host
-  unsigned x, y, z, w;
-};
 
 #include "decima.h"
 #include "engine.h"

@@ -37,7 +37,7 @@ def test_bench_tpch_timed_launch_replay(make, dataset, K, warmup):
     r = cases.case_bench_rollout_sequence(make, dataset, TPCH, B=1024, preroll=1000, warmup=warmup, K=K, stride=64,
                                           expect_resident=True)
     assert r["pending_at_timed_end"] > 0  # the timed launch did preempt steps (completed by the closing launch)
-    assert r["episodes_replayed"] > 16  # the replayed envs crossed episode boundaries
+    assert r["crossed_replayed"] >= 1  # replayed envs crossed episode boundaries (auto-resets inside the sequence)
 
 
 def test_bench_tpch_timed_launch_replay_traced(make, dataset):
