@@ -42,6 +42,6 @@ def test_launcher_two_ranks_host_engine():
 def test_cpu_baseline_worker(workload):
     import bench
 
-    dec, wall, _ = bench._cpu_worker((workload, 3, 1.0, 0.5))
+    dec, wall, _ = bench._cpu_worker((workload, 3, 1.0, 0.5, 0))
     assert dec > 0 and wall >= 1.0
     assert bench.usable_cpus() >= 1 and isinstance(bench.cpu_model(), str)
