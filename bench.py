@@ -341,6 +341,9 @@ def main():
                          "traces would)")
     ap.add_argument("--torch-policy", action="store_true",
                     help="decima workload: run the PyTorch DecimaScheduler instead of the fused kernel")
+    ap.add_argument("--decima-lockstep", action="store_true",
+                    help="decima workload: per decision one fused policy launch + one ssim_step launch for every env "
+                         "(the round-2 path) instead of the persistent Decima rollout (ssim_decima_rollout)")
     ap.add_argument("--ppo-time-limit", type=float, default=0.0,
                     help="ppo workload: override mean_time_limit (ms) of config/decima_tpch.yaml (0 = keep 2e7)")
     ap.add_argument("--lockstep", action="store_true",
@@ -446,6 +449,14 @@ def main():
             pre = 0 if args.no_preempt else _abi.SSIM_ROLLOUT_PREEMPT
             eng.rollout_budget(kind, 1234, 8 * c, B * c, flags=f | pre, time_limits=limits)
 
+    # configs[2] default: the persistent Decima rollout (features + fused policy + step per env in one launch), a
+    # shared budget of B x c decisions per launch, preemptible, auto-reset (the tpch rollout's work sharing)
+    persistent = mode == "decima" and not (args.decima_lockstep or args.torch_policy or host)
+
+    def decima_launch(c, timed):
+        f = _abi.SSIM_ROLLOUT_AUTORESET | _abi.SSIM_ROLLOUT_PREEMPT | (0 if timed else _abi.SSIM_ROLLOUT_WARMUP)
+        eng.decima_rollout(packed, args.seed, 1, 8 * c, B * c, flags=f, time_limits=limits)
+
     def launch_sizes(n, chunk=None):
         chunk = chunk or n
         return [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
@@ -455,11 +466,11 @@ def main():
         stream."""
         if n <= 0:
             return
-        if mode == "rollout":
+        if mode == "rollout" or persistent:
             for i, c in enumerate(launch_sizes(n, chunk)):
                 if events is not None:
                     events[i][0].record(stream)
-                rollout_launch(c, events is not None)
+                (decima_launch if persistent else rollout_launch)(c, events is not None)
                 if events is not None:
                     events[i][1].record(stream)
             return
@@ -492,7 +503,7 @@ def main():
     acc0 = np.array(eng.to_numpy(eng.views["acc"]), dtype=np.int64).copy()
     events = None
     if not host:  # created before the timed region (event creation is host work, not part of a step)
-        n_launch = len(launch_sizes(K, args.chunk or K)) if mode == "rollout" else K
+        n_launch = len(launch_sizes(K, args.chunk or K)) if (mode == "rollout" or persistent) else K
         events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(n_launch)]
     if world > 1:
@@ -527,12 +538,12 @@ def main():
     value = decisions / elapsed
     line = None
     if rank == 0:
-        kernel = "k_rollout" if mode == "rollout" else "k_step"
+        kernel = "k_rollout" if mode == "rollout" else "k_decima_rollout" if persistent else "k_step"
         roofline = None
         if not host and launches:
             kern_ms = kern_ms_sum / world
             achieved = (alg_bytes / world / launches) / (kern_ms / launches / 1e3) / 1e9  # GB/s per GPU
-            traffic, traffic_src, pmc = pmc_traffic(kernel, mode, B, K if mode == "rollout" else 1,
+            traffic, traffic_src, pmc = pmc_traffic(kernel, mode, B, K if (mode == "rollout" or persistent) else 1,
                                                    decisions / world / launches, args.dataset_seed)
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -560,13 +571,14 @@ def main():
             "config": {"workload": wl["desc"].format(B=B), "envs_per_gpu": B,
                        "jobs": cfg["job_arrival_cap"], "executors": cfg["num_executors"],
                        "mean_time_limit": wl["mean_time_limit"], "mode": mode,
-                       "policy": ("torch" if args.torch_policy else "fused HIP kernel") if mode == "decima"
-                       else "device random",
-                       "steps_per_launch": (args.chunk or K) if mode == "rollout" else 1,
+                       "policy": ("torch" if args.torch_policy else "persistent Decima rollout (features + fused "
+                                  "policy + step per env in one launch)" if persistent else "fused HIP kernel")
+                       if mode == "decima" else "device random",
+                       "steps_per_launch": (args.chunk or K) if (mode == "rollout" or persistent) else 1,
                        "work_sharing": ("lockstep" if args.lockstep else "shared budget of envs x steps "
                                         "decisions per launch" + ("" if args.no_preempt else
                                                                   ", preemptible at event boundaries"))
-                       if mode == "rollout" else None,
+                       if (mode == "rollout" or persistent) else None,
                        "preroll": {"bound": preroll, "mean_decisions": float(pre_steps.mean())},
                        "autoreset": bool(mode != "step" and (flags or mode == "decima")),
                        "parallelism": f"env-sharded x{world}",

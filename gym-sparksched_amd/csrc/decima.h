@@ -29,12 +29,25 @@ constexpr int kDecimaMaxDepth = 32;  // edge_mask bits; DAG depth <= max_stages 
 // LDS scratch per env: level i32[S], parent-level bits u32[S], job of node i16[S]
 inline int64_t decima_scratch_bytes(int64_t stage_cap) { return align16(10 * stage_cap); }
 
+// Cross-lane ordering of the scratch updates. LDS scratch (k_decima): the wave's own ds operations are in order, a
+// wave barrier suffices. Global scratch (kGlobal, the persistent Decima rollout: per-env scratch in HBM, too big for
+// the LDS share of 16 waves per CU): a workgroup-scope fence waits for the wave's stores and atomics; the atomics are
+// performed in L2, so every read of an atomically updated word is a W::lds_load (sc0: past the CU's L1).
+template <class W, bool kGlobal>
+__device__ __forceinline__ void scratch_sync() {
+  if constexpr (kGlobal)
+    W::gsync();
+  else
+    W::sync();
+}
+
 template <class W>
 struct DecimaView {
   const ssim_layout& L;
   const uint8_t* obs;
   int eid;
 
+  template <bool kGlobal = false>
   __device__ __forceinline__ void run(float num_tasks_scale, float work_scale, uint8_t* scratch, float* feats,
                                       int32_t* ccap, uint32_t* emask, int32_t* depth_out) const {
     const int S = L.stage_cap, J = L.job_cap, E = L.edge_cap, N = L.num_executors;
@@ -63,7 +76,7 @@ struct DecimaView {
       lev[i] = 0;
       plm[i] = 0u;
     }
-    W::sync();
+    scratch_sync<W, kGlobal>();
     // node features (env_wrapper.py:110-143)
     for (int i = W::lane(); i < n; i += W::kWidth) {
       const int k = job_of[i];
@@ -89,24 +102,29 @@ struct DecimaView {
           changed = true;
         }
       }
-      W::sync();
+      scratch_sync<W, kGlobal>();
       if (!W::ballot(changed)) break;
     }
     int dmax = -1;
-    for (int i = W::lane(); i < n; i += W::kWidth) dmax = lev[i] > dmax ? lev[i] : dmax;
+    for (int i = W::lane(); i < n; i += W::kWidth) {
+      const int l = W::lds_load(lev + i);
+      dmax = l > dmax ? l : dmax;
+    }
     const int depth = W::max_i(dmax) + 1;  // 0 generations for an empty batch
     for (int e = W::lane(); e < ne; e += W::kWidth) {
       const int a = (int)links[2 * e], b = (int)links[2 * e + 1];
-      W::aor(plm + b, 1u << (lev[a] & 31));
+      W::aor(plm + b, 1u << (W::lds_load(lev + a) & 31));
     }
-    W::sync();
+    scratch_sync<W, kGlobal>();
+    const int* plmi = reinterpret_cast<const int*>(plm);
     for (int e = W::lane(); e < ne; e += W::kWidth) {
       const int a = (int)links[2 * e], b = (int)links[2 * e + 1];
-      const uint32_t ma = (1u << (lev[a] & 31)) | plm[a], mb = (1u << (lev[b] & 31)) | plm[b];
+      const uint32_t ma = (1u << (W::lds_load(lev + a) & 31)) | (uint32_t)W::lds_load(plmi + a);
+      const uint32_t mb = (1u << (W::lds_load(lev + b) & 31)) | (uint32_t)W::lds_load(plmi + b);
       em[e] = ma & mb;
     }
     if (W::lane() == 0) depth_out[eid] = depth > kDecimaMaxDepth ? -1 : depth;
-    W::sync();
+    scratch_sync<W, kGlobal>();
   }
 };
 

@@ -139,12 +139,41 @@ struct DecimaPolicyOut {
   float* exec_scores;  // optional [B][N] (k < cap)
 };
 
-// Returns false if the env has more nodes than the LDS plan holds (the caller reports it).
+// The chosen action in registers (wave-uniform), besides the DecimaPolicyOut arrays.
+struct DpAction {
+  int32_t stage_idx, num_exec, job_idx, exec_idx;
+  float lgprob;
+};
+
+// Accumulation into the plan's agg / h_dag / glob rows. LDS plan: ds_add_f32. Global plan (kGlobal): the hardware
+// f32 atomic in L2 (the plan is coarse-grained device memory), not the compare-and-swap loop atomicAdd would emit.
+template <bool kGlobal>
+__device__ __forceinline__ void dp_acc(float* p, float v) {
+  if constexpr (kGlobal)
+    WaveHip::fadd(p, v);  // global_atomic_add_f32, workgroup scope (the plan is the wave's own)
+  else
+    atomicAdd(p, v);
+}
+// A read of an accumulated (atomically updated) plan word: past the L1 on the global plan (wave_hip.h lds_load).
+template <bool kGlobal>
+__device__ __forceinline__ float dp_ld(const float* p) {
+  if constexpr (kGlobal)
+    return WaveHip::ld_rel(p);
+  else
+    return *p;
+}
+
+// Returns false if the env has more nodes than the plan holds (the caller reports it). `lds`: the plan, in LDS
+// (k_decima_policy) or, with kGlobal, a per-env region of global memory (the persistent Decima rollout, whose
+// 16 waves per CU leave no LDS for a J=200 plan); the atomic accumulation phases then end with an agent-scope
+// fence (decima.h scratch_sync). `act` (optional) receives the action.
+template <bool kGlobal = false>
 __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, const uint8_t* __restrict__ obs,
                                          const float* __restrict__ feats, const int32_t* __restrict__ ccap,
                                          const uint32_t* __restrict__ emask, const int32_t* __restrict__ depth,
                                          const float* __restrict__ Wt, int node_cap, uint64_t seed,
-                                         uint64_t counter, int eid, uint8_t* lds, const DecimaPolicyOut& o) {
+                                         uint64_t counter, int eid, uint8_t* lds, const DecimaPolicyOut& o,
+                                         DpAction* act = nullptr) {
   using W = WaveHip;
   const ssim_layout& L = P->L;
   const int S = L.stage_cap, J = L.job_cap, E = L.edge_cap, N = L.num_executors;
@@ -153,7 +182,8 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   const int nj = W::uni(cnt[SSIM_OC_NUM_JOBS]);
   const int lane = W::lane();
   auto out_none = [&]() {
-    if (lane == 0) {
+    if (act != nullptr) *act = DpAction{-1, 1, -1, 0, 0.0f};
+    if (lane == 0 && o.stage_idx != nullptr) {
       o.stage_idx[eid] = -1;
       o.num_exec[eid] = 1;
       o.job_idx[eid] = -1;
@@ -193,9 +223,9 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   for (int i = lane; i < n; i += 64) flag[i] = 0;
   for (int k = lane; k < nj * kDpEmb; k += 64) hdag[k] = 0.0f;
   if (lane < kDpEmb) glob[lane] = 0.0f;
-  W::sync();
+  scratch_sync<W, kGlobal>();
   for (int e = lane; e < ne; e += 64) flag[(int)links[2 * e]] = 1;  // parent has a child
-  W::sync();
+  scratch_sync<W, kGlobal>();
   // h_init = mlp_prep(x); h = h_init (no levels) or mlp_update(h_init) for leaves
   for (int i = lane; i < n; i += 64) {
     float xi[kDecimaFeatures], v[kDpEmb], u[kDpEmb];
@@ -218,7 +248,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
       for (int f = 0; f < kDpEmb; ++f) hh[i * kDpEmb + f] = v[f];
     }
   }
-  W::sync();
+  scratch_sync<W, kGlobal>();
   // message passing, deepest level first (reverse flow: children -> parents)
   for (int lvl = levels - 1; lvl >= 0; --lvl) {
     for (int e = lane; e < ne; e += 64) {  // zero agg and mark dst for the level's parents
@@ -229,7 +259,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
         flag[p] |= 2;
       }
     }
-    W::sync();
+    scratch_sync<W, kGlobal>();
     for (int e = lane; e < ne; e += 64) {  // agg[p] += mlp_msg(h[c]) with the level's old h
       if ((em[e] >> lvl) & 1u) {
         const int p = (int)links[2 * e], c = (int)links[2 * e + 1];
@@ -238,22 +268,22 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
         for (int f = 0; f < kDpEmb; ++f) hc[f] = hh[c * kDpEmb + f];
         dp_mlp<kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffMsg, hc, m);
 #pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) atomicAdd(agg + p * kDpEmb + f, m[f]);
+        for (int f = 0; f < kDpEmb; ++f) dp_acc<kGlobal>(agg + p * kDpEmb + f, m[f]);
       }
     }
-    W::sync();
+    scratch_sync<W, kGlobal>();
     for (int i = lane; i < n; i += 64) {  // h[p] = h_init[p] + mlp_update(agg[p])
       if (flag[i] & 2) {
         float a[kDpEmb], u[kDpEmb];
 #pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) a[f] = agg[i * kDpEmb + f];
+        for (int f = 0; f < kDpEmb; ++f) a[f] = dp_ld<kGlobal>(agg + i * kDpEmb + f);
         dp_mlp<kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffUpd, a, u);
 #pragma unroll
         for (int f = 0; f < kDpEmb; ++f) hh[i * kDpEmb + f] = hi[i * kDpEmb + f] + u[f];
         flag[i] &= 1;
       }
     }
-    W::sync();
+    scratch_sync<W, kGlobal>();
   }
   // DAG and global summaries
   for (int i = lane; i < n; i += 64) {
@@ -265,21 +295,21 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     dp_mlp<kDecimaFeatures + kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffDag, in, v);
     const int g = ndag[i];
 #pragma unroll
-    for (int f = 0; f < kDpEmb; ++f) atomicAdd(hdag + g * kDpEmb + f, v[f]);
+    for (int f = 0; f < kDpEmb; ++f) dp_acc<kGlobal>(hdag + g * kDpEmb + f, v[f]);
   }
-  W::sync();
+  scratch_sync<W, kGlobal>();
   for (int g = lane; g < nj; g += 64) {
     float in[kDpEmb], v[kDpEmb];
 #pragma unroll
-    for (int f = 0; f < kDpEmb; ++f) in[f] = hdag[g * kDpEmb + f];
+    for (int f = 0; f < kDpEmb; ++f) in[f] = dp_ld<kGlobal>(hdag + g * kDpEmb + f);
     dp_mlp<kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffGlob, in, v);
 #pragma unroll
-    for (int f = 0; f < kDpEmb; ++f) atomicAdd(glob + f, v[f]);
+    for (int f = 0; f < kDpEmb; ++f) dp_acc<kGlobal>(glob + f, v[f]);
   }
-  W::sync();
+  scratch_sync<W, kGlobal>();
   float gl[kDpEmb];
 #pragma unroll
-  for (int f = 0; f < kDpEmb; ++f) gl[f] = glob[f];
+  for (int f = 0; f < kDpEmb; ++f) gl[f] = dp_ld<kGlobal>(glob + f);
   // stage scores over schedulable nodes, then a categorical draw (max-shifted softmax, Gumbel-max)
   const uint64_t key = splitmix64(seed ^ splitmix64((uint64_t)eid * 0x9E3779B97F4A7C15ULL + counter));
   float mx = -__builtin_inff(), best = -__builtin_inff();
@@ -293,7 +323,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
 #pragma unroll
       for (int f = 0; f < kDpEmb; ++f) {
         in[kDecimaFeatures + f] = hh[i * kDpEmb + f];
-        in[kDecimaFeatures + kDpEmb + f] = hdag[g * kDpEmb + f];
+        in[kDecimaFeatures + kDpEmb + f] = dp_ld<kGlobal>(hdag + g * kDpEmb + f);
         in[kDecimaFeatures + 2 * kDpEmb + f] = gl[f];
       }
       dp_mlp<kDecimaFeatures + 3 * kDpEmb, 64, 64, 1, true>(Wt + kOffStage, in, &s);
@@ -320,7 +350,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     const int cand = W::bcast_i(pick, W::ffs(m));
     node = cand < node ? cand : node;
   }
-  W::sync();
+  scratch_sync<W, kGlobal>();
   float z = 0.0f;
   int rank = 0;
   for (int i0 = 0; i0 < n; i0 += 64) {  // wave-uniform trip count: ballots need every lane
@@ -340,7 +370,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   for (int f = 0; f < 3; ++f) in[f] = x[p0 * kDecimaFeatures + f];
 #pragma unroll
   for (int f = 0; f < kDpEmb; ++f) {
-    in[3 + f] = hdag[g * kDpEmb + f];
+    in[3 + f] = dp_ld<kGlobal>(hdag + g * kDpEmb + f);
     in[3 + kDpEmb + f] = gl[f];
   }
   float emx = -__builtin_inff(), ebest = -__builtin_inff(), es_k = 0.0f;
@@ -361,7 +391,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     }
   }
   emx = W::max_f(emx);
-  W::sync();
+  scratch_sync<W, kGlobal>();
   float ez = 0.0f;
   for (int k = lane; k < cap; k += 64) ez += expf(escore[k] - emx);
   ez = W::sum_f(ez);
@@ -375,7 +405,8 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     sk = __builtin_bit_cast(float, W::bcast_i(__builtin_bit_cast(int, es_k), l));
   }
   const float lp_exec = ew ? sk - emx - logf(ez) : 0.0f;
-  if (lane == 0) {
+  if (act != nullptr) *act = DpAction{rank, kx + 1, g, kx, lp_stage + lp_exec};
+  if (lane == 0 && o.stage_idx != nullptr) {
     o.stage_idx[eid] = rank;
     o.num_exec[eid] = kx + 1;
     o.job_idx[eid] = g;

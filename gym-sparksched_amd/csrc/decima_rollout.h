@@ -1,0 +1,201 @@
+// decima_rollout.h — persistent Decima rollouts: featurisation, the GNN policy and env.step per env in ONE launch.
+//
+// The reference collects Decima rollouts one env per process (trainers/rollout_worker.py:135-157: per decision
+// DecimaObsWrapper.observation, DecimaScheduler.schedule, env.step). The lockstep GPU collector batches that over
+// envs but pays ~4 launches and a host sync per decision, and every decision waits for the slowest env of the batch.
+// Here each env's wave runs its own loop (kernels.h rollout_body): the Decima features of its current observation
+// (decima.h), the fused policy (decima_policy.h), optionally a copy of the observation / action / reward into a
+// per-env sample arena (the PPO learner's rollout buffer), then the step. No env waits for another; a launch runs
+// whole episodes (collection) or a shared decision budget (benchmark, SSIM_ROLLOUT_PREEMPT | AUTORESET).
+//
+// The features' scratch and the policy's activation plan live in a per-env region of global memory (the
+// workspace): at J = 200 a plan is ~0.7 MB, far above the LDS share of the 16 waves per CU a 4096-env batch runs.
+// Sampling: counter-based Gumbel-max on (seed, env, counter + the env's decision index in its episode), plus the
+// episode number << 32 with auto-reset — the lockstep collector's stream (RolloutCollector: counter = base + k at
+// its k-th step), so both collectors draw the same actions for the same observations.
+#pragma once
+#include "kernels.h"
+#include "decima.h"
+#include "decima_policy.h"
+
+// Per-env global workspace: [features scratch (decima.h) | policy plan for stage_cap nodes (decima_policy.h)], then
+// the feature outputs for all envs (the ssim_decima_features layout).
+struct DecimaWork {
+  int64_t feat_scratch, plan, stride;  // per-env block
+  int64_t feats, ccap, emask, depth, total;  // absolute offsets of the [num_envs] feature arrays
+};
+inline DecimaWork decima_work(const ssim_layout& L) {
+  DecimaWork w{};
+  w.feat_scratch = 0;
+  w.plan = align16(decima_scratch_bytes(L.stage_cap));
+  w.stride = (w.plan + decima_policy_lds_bytes(L.stage_cap, L.job_cap) + 255) & ~int64_t(255);
+  int64_t o = w.stride * L.num_envs;
+  w.feats = o;
+  o = align16(o + (int64_t)L.num_envs * L.stage_cap * kDecimaFeatures * 4);
+  w.ccap = o;
+  o = align16(o + (int64_t)L.num_envs * L.job_cap * 4);
+  w.emask = o;
+  o = align16(o + (int64_t)L.num_envs * L.edge_cap * 4);
+  w.depth = o;
+  o = align16(o + (int64_t)L.num_envs * 4);
+  w.total = o;
+  return w;
+}
+
+struct DecimaRolloutArgs {
+  const float* weights;  // DecimaScheduler.packed_params()
+  uint8_t* work;         // decima_work(L).total bytes
+  DecimaWork wl;
+  float num_tasks_scale, work_scale;
+  uint64_t seed, counter;
+  int32_t autoreset;
+  ssim_decima_samples smp;  // smp.rec == nullptr: no sample arena
+};
+
+struct DecimaPolicy {
+  const Params* P;
+  const uint8_t* obs;
+  DecimaRolloutArgs a;
+
+  template <class S>
+  __device__ __forceinline__ bool act(S& s, int /*k*/, StepIn* out) const {
+    using W = WaveHip;
+    const ssim_layout& L = P->L;
+    const int eid = s.eid;
+    // the collector's episode is over (terminated, truncated by its StochasticTimeLimit, or frozen): no more decisions
+    if (!a.autoreset && (s.h.terminated || s.frozen() || s.h.wall >= s.h.time_limit || s.h.num_jobs == 0))
+      return false;
+    const ssim_decima_samples& sm = a.smp;
+    const int32_t* cnt = reinterpret_cast<const int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
+    const int n = W::uni(cnt[SSIM_OC_NUM_NODES]), ne = W::uni(cnt[SSIM_OC_NUM_EDGES]);
+    const int nj = W::uni(cnt[SSIM_OC_NUM_JOBS]);
+    int32_t* cur = sm.cursor + (int64_t)eid * 8;
+    int cs = 0, cn = 0, ce = 0, cg = 0;
+    if (sm.rec != nullptr) {
+      cs = W::uni(cur[0]);
+      cn = W::uni(cur[1]);
+      ce = W::uni(cur[2]);
+      cg = W::uni(cur[3]);
+      if (cs + 1 > sm.cap_samples || cn + n > sm.cap_nodes || ce + ne > sm.cap_edges || cg + nj > sm.cap_dags) {
+        W::sync();
+        if (W::lane() == 0) cur[4] = 1;  // region full: the host grows the arena and launches again
+        W::sync();
+        return false;
+      }
+    }
+    uint8_t* wk = a.work + (int64_t)eid * a.wl.stride;
+    float* feats = reinterpret_cast<float*>(a.work + a.wl.feats);
+    int32_t* ccap = reinterpret_cast<int32_t*>(a.work + a.wl.ccap);
+    uint32_t* emask = reinterpret_cast<uint32_t*>(a.work + a.wl.emask);
+    int32_t* depth = reinterpret_cast<int32_t*>(a.work + a.wl.depth);
+    DecimaView<W>{L, obs, eid}.template run<true>(a.num_tasks_scale, a.work_scale, wk + a.wl.feat_scratch, feats,
+                                                  ccap, emask, depth);
+    const uint64_t ctr = a.counter + (uint64_t)s.h.decisions + (a.autoreset ? (uint64_t)s.h.episode << 32 : 0ull);
+    DpAction act;
+    const DecimaPolicyOut none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    decima_policy_env<true>(P, obs, feats, ccap, emask, depth, a.weights, L.stage_cap, a.seed, ctr, eid,
+                            wk + a.wl.plan, none, &act);
+    out->stage_idx = act.stage_idx;
+    out->num_exec = act.num_exec;
+    if (sm.rec != nullptr) {  // the observation as the learner's DagBatch rows (schedulers/decima.py build_batch)
+      const float* f = feats + (int64_t)eid * L.stage_cap * kDecimaFeatures;
+      const float* nodes = reinterpret_cast<const float*>(obs + L.ob_nodes) + (int64_t)eid * L.stage_cap * 3;
+      const int64_t* links = reinterpret_cast<const int64_t*>(obs + L.ob_edge_links) + (int64_t)eid * L.edge_cap * 2;
+      const int32_t* ptr = reinterpret_cast<const int32_t*>(obs + L.ob_dag_ptr) + (int64_t)eid * (L.job_cap + 1);
+      const int32_t* cc = ccap + (int64_t)eid * L.job_cap;
+      const uint32_t* em = emask + (int64_t)eid * L.edge_cap;
+      float* xn = sm.nodes + ((int64_t)eid * sm.cap_nodes + cn) * 6;
+      for (int i = W::lane(); i < n; i += W::kWidth) {
+#pragma unroll
+        for (int c = 0; c < kDecimaFeatures; ++c) xn[(int64_t)i * 6 + c] = f[(int64_t)i * kDecimaFeatures + c];
+        xn[(int64_t)i * 6 + 5] = nodes[3 * i + 2];
+      }
+      int32_t* ed = sm.edges + ((int64_t)eid * sm.cap_edges + ce) * 4;
+      for (int e = W::lane(); e < ne; e += W::kWidth) {
+        ed[4 * e + 0] = (int32_t)links[2 * e];
+        ed[4 * e + 1] = (int32_t)links[2 * e + 1];
+        ed[4 * e + 2] = (int32_t)em[e];
+        ed[4 * e + 3] = 0;
+      }
+      int32_t* dg = sm.dags + ((int64_t)eid * sm.cap_dags + cg) * 2;
+      for (int k = W::lane(); k < nj; k += W::kWidth) {
+        dg[2 * k + 0] = ptr[k + 1] - ptr[k];
+        dg[2 * k + 1] = cc[k];
+      }
+      const int dep = W::uni(depth[eid]);
+      W::sync();
+      if (W::lane() == 0) {
+        ssim_decima_sample r;
+        r.num_nodes = n;
+        r.num_edges = ne;
+        r.num_dags = nj;
+        r.depth = dep;
+        r.node_off = cn;
+        r.edge_off = ce;
+        r.dag_off = cg;
+        r.stage_idx = act.stage_idx;
+        r.job_idx = act.job_idx;
+        r.exec_idx = act.exec_idx;
+        r.num_exec = act.num_exec;
+        r.lgprob = act.lgprob;
+        r.wall_before = s.h.wall;
+        r.reward = 0.0;
+        sm.rec[(int64_t)eid * sm.cap_samples + cs] = r;
+        cur[0] = cs + 1;
+        cur[1] = cn + n;
+        cur[2] = ce + ne;
+        cur[3] = cg + nj;
+      }
+      W::sync();
+    }
+    return true;
+  }
+  // the decision's reward (observe() wrote it to the obs arena) into its sample
+  template <class S>
+  __device__ __forceinline__ void done(S& s) const {
+    using W = WaveHip;
+    const ssim_decima_samples& sm = a.smp;
+    if (sm.rec == nullptr) return;
+    const int eid = s.eid;
+    const int cs = W::uni(sm.cursor[(int64_t)eid * 8]);
+    const double r = W::uni(reinterpret_cast<const double*>(obs + P->L.ob_reward)[eid]);
+    W::sync();
+    if (W::lane() == 0 && cs > 0) sm.rec[(int64_t)eid * sm.cap_samples + cs - 1].reward = r;
+    W::sync();
+  }
+};
+
+#ifndef SSIM_DECIMA_ROLLOUT_WAVES
+#define SSIM_DECIMA_ROLLOUT_WAVES 4
+#endif
+template <bool kRes>
+__device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+                                                    DecimaRolloutArgs a, int num_steps, int flags,
+                                                    const double* __restrict__ limits, uint8_t* reset,
+                                                    int32_t* action_log, int64_t budget) {
+  a.autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
+  const DecimaPolicy pol{P, obs, a};
+  rollout_body<kRes, 0, 0, 0>(P, state, obs, pol, num_steps, flags, limits, reset, action_log, nullptr, budget,
+                              nullptr);
+}
+template <bool kRes>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_DECIMA_ROLLOUT_WAVES))) void k_decima_rollout(
+    const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
+    const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget) {
+  decima_rollout_body<kRes>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget);
+}
+// launches that are not measured (SSIM_ROLLOUT_WARMUP), under their own symbol
+template <bool kRes>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_DECIMA_ROLLOUT_WAVES))) void k_decima_rollout_warmup(
+    const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
+    const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget) {
+  decima_rollout_body<kRes>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget);
+}
+
+using DecimaRolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, DecimaRolloutArgs, int, int, const double*,
+                                 uint8_t*, int32_t*, int64_t);
+struct DecimaRolloutSet {
+  DecimaRolloutFn rollout, rollout_warmup;
+};
+DecimaRolloutSet decima_rollout_hbm();  // k_dr_hbm.hip
+DecimaRolloutSet decima_rollout_lds();  // k_dr_lds.hip

@@ -243,6 +243,9 @@ struct Sim {
 #ifndef SSIM_EV_PAGES_GENERIC
 #define SSIM_EV_PAGES_GENERIC 1
 #endif
+#ifndef SSIM_DUR_CACHE
+#define SSIM_DUR_CACHE 1
+#endif
   static constexpr int kEvPages = W::kWidth == 64 ? (kN > 0 ? (kN + 63) / 64 : SSIM_EV_PAGES_GENERIC) : 0;
   struct EvRegs {
     uint32_t tlo, thi;  // ev_t bits (+inf: no event)
@@ -251,6 +254,14 @@ struct Sim {
   };
   EvRegs evr[kEvPages > 0 ? kEvPages : 1];
   __device__ __forceinline__ bool ev_in_regs() const { return kEvPages > 0 && NE <= 64 * kEvPages; }
+  // Duration-descriptor cache (kernels specialised on <= 16 executors): per executor, the (wave x exec-level)
+  // duration-list descriptors of the stage its current task runs on (24 lanes x {len, off}, as dur_gather) in the
+  // wave's LDS scratch (StateOffsets::sc_dcache). A task completion whose stage has tasks left runs the next task on
+  // the same stage (spark_sched_sim.py:466-470), so the pop reads its descriptors from LDS together with the stage and
+  // executor records instead of issuing the dataset gather whose latency the draw then waits on. Filled at every other
+  // task start (run_next_task) and for the pending tasks when a launch starts (ev_regs_load). (Kept in LDS: as a
+  // register array in the Sim object it pushed the whole object into scratch memory.)
+  static constexpr bool kDurCache = W::kWidth == 64 && kN > 0 && kN <= kDurCacheMaxExecs && SSIM_DUR_CACHE;
   const HotParams* HPp;  // host build: Params::hp read in place
   uint32_t hpv;          // device: dword `lane` of Params::hp
 #ifdef SSIM_PROFILE
@@ -1054,6 +1065,14 @@ struct Sim {
         evr[p].ts = ((int32_t)r.ev_type << 16) | (uint16_t)r.ev_stage;
       }
     }
+    if constexpr (kDurCache) {  // the pending tasks' descriptors (independent gathers, one latency)
+      for (int e = 0; e < kN; ++e) {
+        const ExecRec x = ld_rec(exr(e));
+        const bool task = x.ev_seq >= 0 && x.ev_type == kEvTask && x.ev_stage >= 0;
+        const int ts = task ? (int)W::uni(stage(x.ev_stage).ts) : 0;
+        dcache_store(e, dur_gather(ts));
+      }
+    }
   }
   __device__ __forceinline__ void ev_regs_set(int e, double t, int seq, int type, int g) {
     if constexpr (kEvPages > 0) {
@@ -1118,6 +1137,21 @@ struct Sim {
   struct DurDesc {
     int len, off;  // this lane's descriptor (device) — unused by a 1-lane build
   };
+  struct alignas(8) DescPair {
+    int32_t len, off;
+  };
+  __device__ __forceinline__ void dcache_store(int e, const DurDesc& d) {
+    if (W::lane() < 24) S<DescPair>(O.sc_dcache)[e * 24 + W::lane()] = DescPair{d.len, d.off};
+  }
+  __device__ __forceinline__ DurDesc dcache_load(int e) const {
+    DurDesc d{0, 0};
+    if (W::lane() < 24) {
+      const DescPair v = S<DescPair>(O.sc_dcache)[e * 24 + W::lane()];
+      d.len = v.len;
+      d.off = v.off;
+    }
+    return d;
+  }
   __device__ __forceinline__ DurDesc dur_gather(int ts) const {
     DurDesc d{0, 0};
     if (W::kWidth >= 24) {
@@ -1331,7 +1365,9 @@ struct Sim {
     const ExecRec xraw = exr(e);
     StageRec s = ld_rec(sraw);
     ExecRec x = ld_rec(xraw);
-    run_next_task_rec(e, g, s, x);
+    const DurDesc dd = dur_gather(s.ts);
+    if constexpr (kDurCache) dcache_store(e, dd);
+    run_next_task_rec(e, g, s, x, dd);
     stage(g) = s;
     exr(e) = x;
   }
@@ -1700,13 +1736,19 @@ struct Sim {
           on_executor_arrival(e, g);
           SSIM_TOC(t_x, kPhExecArr);
         } else {
-          // the stage and executor records are read together (one LDS round trip), then made uniform
+          // the stage and executor records (and the cached duration descriptors) are read together (one LDS round
+          // trip), then made uniform
           const StageRec sraw = stage(g);
           const ExecRec xraw = exr(e);
+          DurDesc ddc{0, 0};
+          if constexpr (kDurCache) ddc = dcache_load(e);
           const StageRec sr = ld_rec(sraw);
+          if constexpr (!kDurCache) {
+            if (sr.rem > 0) ddc = dur_gather(sr.ts);
+          }
           // the next task's duration descriptors (if the stage has tasks left): issued now, used after the job
           // record read
-          on_task_done(e, g, sr, ld_rec(xraw), sr.rem > 0 ? dur_gather(sr.ts) : DurDesc{0, 0});
+          on_task_done(e, g, sr, ld_rec(xraw), ddc);
           SSIM_TOC(t_x, kPhTaskDone);
         }
       }

@@ -1,0 +1,5 @@
+// k_dr_lds.hip — persistent Decima rollout (decima_rollout.h): hot block LDS-resident (small batches, e.g. the 16 envs
+// of a decima_tpch.yaml PPO iteration, one env per CU with the opt-in 160 KB of LDS).
+#include "decima_rollout.h"
+
+DecimaRolloutSet decima_rollout_lds() { return {k_decima_rollout<true>, k_decima_rollout_warmup<true>}; }

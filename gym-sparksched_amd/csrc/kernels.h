@@ -90,9 +90,24 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
   s.save_hot();
 }
 
-template <bool kRes, int kN, int kJ, int kS>
+// The action driver of a fused rollout: `act` chooses the next action of the env (false: the env takes no more
+// decisions in this launch, e.g. the Decima collector's episode ended or its sample arena is full), `done` runs after
+// a decision this launch started has completed (its observation written).
+struct HeuristicPolicy {  // fair / FIFO / random (policy.h)
+  int kind;
+  uint64_t seed;
+  template <class S>
+  __device__ __forceinline__ bool act(S& s, int /*k*/, StepIn* a) const {
+    *a = sim_policy(s, kind, seed);
+    return true;
+  }
+  template <class S>
+  __device__ __forceinline__ void done(S&) const {}
+};
+
+template <bool kRes, int kN, int kJ, int kS, class Pol>
 __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
-                                                int kind, uint64_t seed, int num_steps, int flags,
+                                                const Pol& pol, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
                                                 int32_t* action_log, uint64_t* prof_out, int64_t budget,
                                                 const int32_t* __restrict__ env_steps) {
@@ -162,7 +177,8 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
         if (granted == 0 && (granted = stop.claim(B, last)) == 0) break;
         --granted;
       }
-      const StepIn a = sim_policy(s, kind, seed);
+      StepIn a;
+      if (!pol.act(s, k, &a)) break;
 #ifdef SSIM_PROFILE
       s.prof_add(kPhPolicy, WaveHip::clock() - t0);
 #endif
@@ -173,8 +189,12 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
       ++k;
       WaveHip::sync();
       simulate = s.step_begin(a, &st0);
+      if (!simulate) pol.done(s);
     }
-    if (simulate && !s.finish_step(st0, stop)) break;  // preempted mid-simulation: pending until the next launch
+    if (simulate) {
+      if (!s.finish_step(st0, stop)) break;  // preempted mid-simulation: pending until the next launch
+      pol.done(s);
+    }
 #ifdef SSIM_PROFILE
     {
       const uint64_t dc = WaveHip::clock() - t0;
@@ -203,16 +223,17 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
   const Params *__restrict__ P, uint8_t *state, uint8_t *obs, int kind, uint64_t seed, int num_steps, int flags, \
       const double *__restrict__ limits, uint8_t *reset, int32_t *action_log, uint64_t *prof_out, int64_t budget, \
       const int32_t *__restrict__ env_steps
-#define SSIM_ROLLOUT_PASS P, state, obs, kind, seed, num_steps, flags, limits, reset, action_log, prof_out, budget, env_steps
 template <bool kRes, int kN, int kJ, int kS>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_ROLLOUT_WAVES))) void k_rollout(SSIM_ROLLOUT_ARGS) {
-  rollout_body<kRes, kN, kJ, kS>(SSIM_ROLLOUT_PASS);
+  rollout_body<kRes, kN, kJ, kS>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags, limits, reset, action_log,
+                                 prof_out, budget, env_steps);
 }
 // The same rollout under its own symbol for launches that are not measured (SSIM_ROLLOUT_WARMUP: a benchmark's
 // pre-roll and warm-up), so a profiler's per-kernel statistics of k_rollout cover the timed launches only.
 template <bool kRes, int kN, int kJ, int kS>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_ROLLOUT_WAVES))) void k_rollout_warmup(SSIM_ROLLOUT_ARGS) {
-  rollout_body<kRes, kN, kJ, kS>(SSIM_ROLLOUT_PASS);
+  rollout_body<kRes, kN, kJ, kS>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags, limits, reset, action_log,
+                                 prof_out, budget, env_steps);
 }
 
 using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);

@@ -142,7 +142,8 @@ struct StateOffsets {
       sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/;
   int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
-      sc_row_of /*int16[S]*/, sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build only*/;
+      sc_row_of /*int16[S]*/, sc_dcache /*int32x2[N][24] when N <= kDurCacheMaxExecs*/,
+      sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build only*/;
 };
 
 constexpr int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
@@ -153,6 +154,7 @@ constexpr int set_cap_for(int n) {  // smallest power of two > 4N (max CPython s
   return c;
 }
 constexpr int commit_cap_for(int n) { return 2 * n + 2; }
+constexpr int64_t kDurCacheMaxExecs = 16;
 
 // The per-env block layout as a function of (N, J, S). Single source of truth for the host layout and for
 // the device engine, which re-derives it with N and J as compile-time constants where it can.
@@ -211,6 +213,8 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   s = align16(s + T);
   O.sc_row_of = s;
   s = align16(s + 2 * S);
+  O.sc_dcache = s;  // engine.h duration-descriptor cache (kernels specialised on few executors)
+  s = align16(s + (N <= kDurCacheMaxExecs ? 8 * 24 * N : 0));
   O.sc_prof = s;
 #ifdef SSIM_PROFILE
   s += 8 * 64;

@@ -15,6 +15,7 @@
 #include "kernels.h"
 #include "decima.h"
 #include "decima_policy.h"
+#include "decima_rollout.h"
 
 // ------------------------------------------------------------------------------------------ kernels
 
@@ -414,6 +415,64 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
                      h->obs, node_feats, commit_cap, edge_mask, depth, params, node_cap, seed, counter, env_mask, o,
                      overflow);
   return hip_check(hipGetLastError(), "k_decima_policy launch");
+}
+
+extern "C" int64_t ssim_decima_workspace_bytes(const ssim_handle* h) {
+  if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_decima_workspace_bytes: null handle");
+  return decima_work(h->params.L).total;
+}
+
+extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t num_params, float num_tasks_scale,
+                                   float work_scale, uint64_t seed, uint64_t counter, int32_t max_steps,
+                                   int64_t total_decisions, int32_t flags, const double* time_limits, void* workspace,
+                                   int64_t workspace_bytes, const ssim_decima_samples* samples, int32_t* action_log,
+                                   void* stream) {
+  if (h == nullptr || params == nullptr || workspace == nullptr || max_steps < 0 || total_decisions < 0)
+    return set_err(SSIM_E_ARG, "ssim_decima_rollout: bad argument");
+  if (num_params != kDecimaParams)
+    return set_err(SSIM_E_ARG, "ssim_decima_rollout: %d parameters, the fused kernel implements the "
+                   "decima_tpch.yaml architecture (%d)", num_params, kDecimaParams);
+  if ((flags & ~(SSIM_ROLLOUT_AUTORESET | SSIM_ROLLOUT_PREEMPT | SSIM_ROLLOUT_WARMUP)) != 0)
+    return set_err(SSIM_E_ARG, "ssim_decima_rollout: unknown flags 0x%x", flags);
+  if ((flags & SSIM_ROLLOUT_PREEMPT) && total_decisions <= 0)
+    return set_err(SSIM_E_ARG, "ssim_decima_rollout: SSIM_ROLLOUT_PREEMPT needs a decision budget");
+  if ((flags & SSIM_ROLLOUT_AUTORESET) && !(h->params.C.job_arrival_gap > 0.0))
+    return set_err(SSIM_E_ARG, "ssim_decima_rollout: auto-reset needs job_arrival_gap in the config");
+  const ssim_layout& L = h->params.L;
+  if (h->params.C.max_stages > kDecimaMaxDepth)
+    return set_err(SSIM_E_ARG, "ssim_decima_rollout: max_stages %d > %d (edge-mask word)", h->params.C.max_stages,
+                   kDecimaMaxDepth);
+  if (L.num_executors > 64 * kDpExecChunks)
+    return set_err(SSIM_E_ARG, "ssim_decima_rollout: more than %d executors", 64 * kDpExecChunks);
+  const DecimaWork wl = decima_work(L);
+  if (workspace_bytes < wl.total)
+    return set_err(SSIM_E_ARG, "ssim_decima_rollout: workspace of %lld B, needs %lld (ssim_decima_workspace_bytes)",
+                   (long long)workspace_bytes, (long long)wl.total);
+  DecimaRolloutArgs a{};
+  a.weights = params;
+  a.work = static_cast<uint8_t*>(workspace);
+  a.wl = wl;
+  a.num_tasks_scale = num_tasks_scale;
+  a.work_scale = work_scale;
+  a.seed = seed;
+  a.counter = counter;
+  if (samples != nullptr) {
+    const ssim_decima_samples& sm = *samples;
+    if (sm.cursor == nullptr || sm.rec == nullptr || sm.nodes == nullptr || sm.edges == nullptr || sm.dags == nullptr ||
+        sm.cap_samples <= 0 || sm.cap_nodes < 0 || sm.cap_edges < 0 || sm.cap_dags < 0)
+      return set_err(SSIM_E_ARG, "ssim_decima_rollout: incomplete sample arena");
+    a.smp = sm;
+  }
+  const DecimaRolloutSet ks = h->params.O.lds_resident ? decima_rollout_lds() : decima_rollout_hbm();
+  const DecimaRolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
+  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  if (rc != SSIM_OK) return rc;
+  if (total_decisions > 0 && h->ticket_slot) flags |= kFlagTicketSlot;
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream, dparams(h),
+                     h->state, h->obs, a, max_steps, flags, time_limits, h->reset, action_log, total_decisions);
+  const int rc2 = hip_check(hipGetLastError(), "k_decima_rollout launch");
+  if (rc2 == SSIM_OK && total_decisions > 0) h->ticket_slot ^= 1;
+  return rc2;
 }
 
 extern "C" const char* ssim_last_error(void) { return g_err; }

@@ -159,11 +159,28 @@ struct WaveHip {
   // streaming (non-temporal) global store
   template <class T>
   __device__ static __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
-  // LDS atomics / loads for lane-parallel relaxations
-  __device__ static __forceinline__ int lds_load(const int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
-  __device__ static __forceinline__ void amax(int* p, int v) { atomicMax(p, v); }
-  __device__ static __forceinline__ void amin(int* p, int v) { atomicMin(p, v); }
-  __device__ static __forceinline__ void aor(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+  // Atomics / loads for lane-parallel relaxations over LDS or a wave's own global scratch: workgroup scope (the data
+  // is private to the wave). On global memory the atomics are performed in L2 and the load carries sc0 (it bypasses
+  // the CU's L1), so it sees them; system / agent scope would take the atomics to memory and make fences write back
+  // and invalidate the L2.
+  __device__ static __forceinline__ int lds_load(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ static __forceinline__ float ld_rel(const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ static __forceinline__ void amax(int* p, int v) {
+    __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ static __forceinline__ void amin(int* p, int v) {
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ static __forceinline__ void aor(uint32_t* p, uint32_t v) {
+    __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ static __forceinline__ void fadd(float* p, float v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   __device__ static __forceinline__ float max_f(float x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

@@ -104,5 +104,22 @@ class SsimLayout(ct.Structure):
         "ob_reward", "ob_wall_time", "ob_acc", "ob_trace")]
 
 
+class SsimDecimaSamples(ct.Structure):
+    """ssim_decima_samples: the persistent Decima rollout's per-env sample arena (device pointers)."""
+    _fields_ = [("cursor", ct.c_void_p), ("rec", ct.c_void_p), ("nodes", ct.c_void_p), ("edges", ct.c_void_p),
+                ("dags", ct.c_void_p), ("cap_samples", ct.c_int32), ("cap_nodes", ct.c_int32),
+                ("cap_edges", ct.c_int32), ("cap_dags", ct.c_int32)]
+
+
+# ssim_decima_sample (64 B): int32 fields, then float lgprob, then f64 wall_before / reward
+SAMPLE_I32 = ["num_nodes", "num_edges", "num_dags", "depth", "node_off", "edge_off", "dag_off", "stage_idx",
+              "job_idx", "exec_idx", "num_exec"]
+SAMPLE_BYTES = 64
+SAMPLE_LGPROB = 11  # float32 word index
+SAMPLE_WALL, SAMPLE_REWARD = 6, 7  # float64 word indices
+CURSOR_WORDS = 8
+CUR_SAMPLES, CUR_NODES, CUR_EDGES, CUR_DAGS, CUR_FULL = range(5)
+
+
 def layout_dict(layout: SsimLayout) -> dict:
     return {name: getattr(layout, name) for name, _ in SsimLayout._fields_}

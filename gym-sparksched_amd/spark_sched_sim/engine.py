@@ -376,6 +376,36 @@ class DeviceEngine:
             "ssim_decima_features")
         return d
 
+    def decima_workspace(self):
+        """The persistent Decima rollout's per-env workspace (ssim_decima_workspace_bytes), allocated once."""
+        if getattr(self, "_dws", None) is None:
+            n = int(self._native.lib().ssim_decima_workspace_bytes(self.handle))
+            if n <= 0:
+                self._native.check(-1, "ssim_decima_workspace_bytes")
+            self._dws = self.torch.zeros(n, dtype=self.torch.uint8, device=self.device)
+        return self._dws
+
+    def decima_rollout(self, params, seed: int, counter: int, max_steps: int, total_decisions: int = 0,
+                       flags: int = 0, time_limits=None, samples=None, action_log=None,
+                       num_tasks_scale: float = 200.0, work_scale: float = 1e5):
+        """ssim_decima_rollout: Decima features + fused policy + step per env and decision, in ONE launch.
+        params: DecimaScheduler.packed_params() (fp32 device tensor). samples: a DecimaSampleArena (or None).
+        flags: 0 = collect until each env's episode ends; _abi.SSIM_ROLLOUT_AUTORESET / PREEMPT (with
+        total_decisions) / WARMUP as ssim_rollout_budget."""
+        ws = self.decima_workspace()
+        tl = None
+        if time_limits is not None:
+            tl = self.torch.as_tensor(np.asarray(time_limits, dtype=np.float64).reshape(self.num_envs),
+                                      device=self.device) if not hasattr(time_limits, "data_ptr") else time_limits
+        st = samples.struct() if samples is not None else None
+        self._keep_dr = (params, tl, st)
+        self._native.check(self._native.lib().ssim_decima_rollout(
+            self.handle, params.data_ptr(), params.numel(), float(num_tasks_scale), float(work_scale),
+            int(seed) & (2**64 - 1), int(counter) & (2**64 - 1), int(max_steps), int(total_decisions), int(flags),
+            None if tl is None else tl.data_ptr(), ws.data_ptr(), ws.numel(),
+            None if st is None else ct.byref(st), None if action_log is None else action_log.data_ptr(),
+            self._stream()), "ssim_decima_rollout")
+
     def decima_features_np(self, num_tasks_scale: float = 200.0, work_scale: float = 1e5) -> dict:
         return {k: x.cpu().numpy() for k, x in self.decima_features(num_tasks_scale, work_scale).items()}
 

@@ -43,10 +43,14 @@ def lib() -> ct.CDLL:
                                      vp]
     L.ssim_job_times.argtypes = [vp, vp, vp, vp, vp]
     L.ssim_decima_features.argtypes = [vp, ct.c_float, ct.c_float, vp, vp, vp, vp, vp]
+    L.ssim_decima_workspace_bytes.argtypes = [vp]
+    L.ssim_decima_workspace_bytes.restype = ct.c_int64
+    L.ssim_decima_rollout.argtypes = [vp, vp, i32, ct.c_float, ct.c_float, u64, u64, i32, ct.c_int64, i32, vp, vp,
+                                      ct.c_int64, vp, vp, vp]
     L.ssim_last_error.restype = ct.c_char_p
     for name in ("ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
                  "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
-                 "ssim_job_times", "ssim_decima_features", "ssim_decima_policy"):
+                 "ssim_job_times", "ssim_decima_features", "ssim_decima_policy", "ssim_decima_rollout"):
         getattr(L, name).restype = ct.c_int
     _lib = L
     return L
@@ -60,4 +64,5 @@ def check(rc: int, what: str) -> None:
 EXPORTED_SYMBOLS = ["ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
                     "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
                     "ssim_job_times",
-                    "ssim_decima_features", "ssim_decima_policy", "ssim_last_error"]
+                    "ssim_decima_features", "ssim_decima_policy", "ssim_decima_workspace_bytes", "ssim_decima_rollout",
+                    "ssim_last_error"]

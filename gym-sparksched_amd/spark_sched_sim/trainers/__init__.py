@@ -5,4 +5,5 @@ Restates trainers/{trainer,ppo,rollout_worker}.py and trainers/utils/{returns_ca
 
 from .ppo import DECIMA_TPCH, PPO, make_trainer  # noqa: F401
 from .returns import Baseline, ReturnsCalculator  # noqa: F401
-from .rollouts import AsyncRolloutCollector, GpuRolloutBuffer, RolloutCollector  # noqa: F401
+from .rollouts import (AsyncRolloutCollector, ArenaRolloutBuffer, DecimaSampleArena, DeviceRolloutCollector,  # noqa: F401
+                       GpuRolloutBuffer, RolloutCollector)

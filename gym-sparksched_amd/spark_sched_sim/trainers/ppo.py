@@ -30,7 +30,7 @@ import torch
 from ..distributed import all_gather_var, gather_var, split_rows
 from ..schedulers.decima import DagBatch, DecimaScheduler, cat_batches, select_envs
 from .returns import Baseline, ReturnsCalculator
-from .rollouts import AsyncRolloutCollector, RolloutCollector
+from .rollouts import AsyncRolloutCollector, DeviceRolloutCollector, RolloutCollector
 
 EPS = 1e-8  # ppo.py:13
 _BATCH_TENSORS = ["x", "edge_index", "edge_bits", "env_levels", "ptr", "node_dag", "node_env", "dag_env", "obs_ptr",
@@ -128,6 +128,12 @@ class PPO:
                                                    seed=rseed, row_offset=self.row_lo)
         else:
             self.collector = RolloutCollector(self.engine, self.scheduler, seed=rseed, row_offset=self.row_lo)
+            # device engines: the whole collection in one persistent launch (same actions, csrc/decima_rollout.h);
+            # train_cfg["lockstep_rollouts"] keeps the per-decision collector
+            if (self.collector.on_device and self.collector.fused and hasattr(self.engine, "decima_rollout")
+                    and not train_cfg.get("lockstep_rollouts", False)):
+                self.collector = DeviceRolloutCollector(self.engine, self.scheduler, seed=rseed,
+                                                        row_offset=self.row_lo)
         self.gen = torch.Generator(device=self.device).manual_seed(rseed)  # learner's minibatch shuffling
         self.time_limit_rngs = None
         if self.mean_time_limit:
@@ -169,9 +175,10 @@ class PPO:
         go to the learner (rank 0) only, None elsewhere."""
         times, rewards, lengths, sample = buf.trajectories()
         obs, acts = buf.samples()
-        canon = sample[sample >= 0]  # row-major: row r's decisions in order, rows ascending
-        obs = select_envs(obs, canon)
-        acts = {k: v[canon] for k, v in acts.items()}
+        if not getattr(buf, "row_major", False):
+            canon = sample[sample >= 0]  # row-major: row r's decisions in order, rows ascending
+            obs = select_envs(obs, canon)
+            acts = {k: v[canon] for k, v in acts.items()}
         if self.world > 1:
             T = torch.tensor([rewards.shape[1]], dtype=torch.int64, device=rewards.device)
             Tm = int(max(int(t.item()) for t in all_gather_var(T, self.world)))

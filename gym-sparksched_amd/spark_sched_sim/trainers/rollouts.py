@@ -212,6 +212,179 @@ class RolloutCollector:
         return buf
 
 
+class DecimaSampleArena:
+    """Device sample arena of the persistent Decima rollout (include/sparksched.h ssim_decima_samples): per env, one
+    64-B record per decision and the decision's observation as node / edge / DAG rows. Regions grow (doubling, the
+    used prefix copied) when the kernel reports one full; the env then continues where it stopped."""
+
+    def __init__(self, num_envs: int, device, cap_samples: int = 1024, cap_nodes: int = 1 << 16,
+                 cap_edges: int = 1 << 16, cap_dags: int = 1 << 14):
+        self.B = num_envs
+        self.device = device
+        i32 = dict(dtype=torch.int32, device=device)
+        self.cursor = torch.zeros((num_envs, _abi.CURSOR_WORDS), **i32)
+        self.caps = [int(cap_samples), int(cap_nodes), int(cap_edges), int(cap_dags)]
+        self.rec = torch.zeros((num_envs, self.caps[0], _abi.SAMPLE_BYTES // 4), **i32)
+        self.nodes = torch.zeros((num_envs, self.caps[1], 6), dtype=torch.float32, device=device)
+        self.edges = torch.zeros((num_envs, self.caps[2], 4), **i32)
+        self.dags = torch.zeros((num_envs, self.caps[3], 2), **i32)
+
+    def struct(self) -> _abi.SsimDecimaSamples:
+        return _abi.SsimDecimaSamples(self.cursor.data_ptr(), self.rec.data_ptr(), self.nodes.data_ptr(),
+                                      self.edges.data_ptr(), self.dags.data_ptr(), *self.caps)
+
+    def clear(self) -> None:
+        self.cursor.zero_()
+
+    @staticmethod
+    def _grown(t: torch.Tensor, cap: int) -> torch.Tensor:
+        out = torch.zeros((t.shape[0], cap) + tuple(t.shape[2:]), dtype=t.dtype, device=t.device)
+        out[:, : t.shape[1]] = t
+        return out
+
+    def grow(self, cur: np.ndarray) -> None:
+        """After a launch that left envs with the full flag: double the regions that are >= 3/4 used by a full env
+        (all of them if none is), then clear the flags."""
+        full = cur[:, _abi.CUR_FULL] != 0
+        used = cur[full][:, [_abi.CUR_SAMPLES, _abi.CUR_NODES, _abi.CUR_EDGES, _abi.CUR_DAGS]].max(axis=0)
+        big = [u * 4 >= 3 * c for u, c in zip(used, self.caps)]
+        if not any(big):
+            big = [True] * 4
+        names = ["rec", "nodes", "edges", "dags"]
+        for i, b in enumerate(big):
+            if b:
+                self.caps[i] *= 2
+                setattr(self, names[i], self._grown(getattr(self, names[i]), self.caps[i]))
+        self.cursor[:, _abi.CUR_FULL] = 0
+
+    def buffer(self, final_wall: torch.Tensor) -> "ArenaRolloutBuffer":
+        return ArenaRolloutBuffer(self, final_wall)
+
+
+class ArenaRolloutBuffer:
+    """GpuRolloutBuffer's interface over a DecimaSampleArena: samples in env-major order (env 0's decisions in
+    order, then env 1's, ...), built into one DagBatch with a fixed number of launches (no per-step batches)."""
+
+    row_major = True  # samples() is already in (row, decision) order
+
+    def __init__(self, arena: DecimaSampleArena, final_wall: torch.Tensor):
+        self.arena = arena
+        self.num_envs = arena.B
+        self.final_wall = final_wall
+        self.lengths = arena.cursor[:, _abi.CUR_SAMPLES].long()
+        self._n = int(self.lengths.sum().item())
+        self._rows = None
+
+    def __len__(self) -> int:
+        return self._n
+
+    def _sample_rows(self):
+        """(env, k) of every sample in env-major order and its record fields."""
+        if self._rows is None:
+            a = self.arena
+            B = self.num_envs
+            dev = a.cursor.device
+            env = torch.repeat_interleave(torch.arange(B, device=dev), self.lengths, output_size=self._n)
+            k = torch.arange(self._n, device=dev) - (torch.cumsum(self.lengths, 0) - self.lengths)[env]
+            rec = a.rec[env, k]  # [n, 16] int32 words
+            self._rows = (env, k, rec)
+        return self._rows
+
+    def trajectories(self):
+        B = self.num_envs
+        dev = self.final_wall.device
+        env, k, rec = self._sample_rows()
+        T = int(self.lengths.max().item()) if self._n else 0
+        f64 = rec.view(torch.float64)  # [n, 8]
+        times = torch.zeros((B, T + 1), dtype=torch.float64, device=dev)
+        rewards = torch.zeros((B, T), dtype=torch.float64, device=dev)
+        times[env, k] = f64[:, _abi.SAMPLE_WALL]
+        rewards[env, k] = f64[:, _abi.SAMPLE_REWARD]
+        times[torch.arange(B, device=dev), self.lengths] = self.final_wall.double()
+        sample = torch.full((B, T), -1, dtype=torch.long, device=dev)
+        sample[env, k] = torch.arange(self._n, device=dev)
+        return times, rewards, self.lengths, sample
+
+    def samples(self):
+        from ..schedulers.decima import _expand, _excl, _ptr
+
+        a = self.arena
+        env, _, rec = self._sample_rows()
+        dev = rec.device
+        f = {name: rec[:, i].long() for i, name in enumerate(_abi.SAMPLE_I32)}
+        n, ne, nj = f["num_nodes"], f["num_edges"], f["num_dags"]
+        Ns = self._n
+        if Ns:
+            Nt, Et, Gt, L, Nmax = (int(v) for v in torch.stack(
+                [n.sum(), ne.sum(), nj.sum(), (torch.clamp(f["depth"] - 1, min=0) * (n > 0)).max(),
+                 n.max()]).tolist())
+        else:
+            Nt = Et = Gt = L = Nmax = 0
+        node_s, nl = _expand(n, Nt)
+        node_src = env[node_s] * a.caps[1] + f["node_off"][node_s] + nl
+        rows = a.nodes.reshape(-1, 6)[node_src]
+        edge_s, el = _expand(ne, Et)
+        edge_src = env[edge_s] * a.caps[2] + f["edge_off"][edge_s] + el
+        erows = a.edges.reshape(-1, 4)[edge_src]
+        dag_s, dl = _expand(nj, Gt)
+        dag_src = env[dag_s] * a.caps[3] + f["dag_off"][dag_s] + dl
+        drows = a.dags.reshape(-1, 2)[dag_src].long()
+        node_base = _excl(n)
+        stage_mask = rows[:, 5] != 0
+        node_dag, _ = _expand(drows[:, 0], Nt)
+        from ..schedulers.decima import DagBatch
+
+        batch = DagBatch(
+            x=rows[:, :5].contiguous(),
+            edge_index=(erows[:, :2].long() + node_base[edge_s][:, None]).t().contiguous(),
+            edge_bits=erows[:, 2].contiguous(), max_levels=L,
+            env_levels=torch.clamp(f["depth"] - 1, min=0) * (n > 0), ptr=_ptr(drows[:, 0]), node_dag=node_dag,
+            node_env=node_s, dag_env=dag_s, obs_ptr=_ptr(nj), stage_mask=stage_mask, exec_cap=drows[:, 1],
+            num_stage_acts=torch.zeros(Ns, dtype=torch.long, device=dev).index_add_(0, node_s, stage_mask.long()),
+            num_nodes=n, num_edges=ne, num_envs=Ns, max_nodes=Nmax)
+        acts = {"stage_idx": f["stage_idx"], "job_idx": f["job_idx"], "exec_idx": f["exec_idx"],
+                "lgprob": rec[:, _abi.SAMPLE_LGPROB].view(torch.float32).contiguous()}
+        return batch, acts
+
+
+class DeviceRolloutCollector(RolloutCollector):
+    """RolloutWorkerSync.collect_rollout (rollout_worker.py:135-157) for every row at once in ONE kernel launch
+    (ssim_decima_rollout, csrc/decima_rollout.h): each env's wave runs its own decision loop (features, fused Decima
+    policy, step) until its episode ends and leaves every decision in a DecimaSampleArena. Same sampling stream as
+    RolloutCollector's fused path (counter = call << 32 + decision index + 1, keyed by the global row), so both draw
+    the same actions from the same observations."""
+
+    def __init__(self, engine, policy, **kw):
+        super().__init__(engine, policy, **kw)
+        if not (self.on_device and self.fused):
+            raise ValueError("DeviceRolloutCollector needs a DeviceEngine and the decima_tpch.yaml architecture")
+        self.arena = DecimaSampleArena(engine.num_envs, engine.device)
+        self.launches = 0
+
+    @torch.no_grad()
+    def collect(self, seeds, time_limits=None, generator=None, max_steps: int = 10**9) -> ArenaRolloutBuffer:
+        self.calls += 1
+        eng = self.engine
+        B = eng.num_envs
+        limits = None if time_limits is None else np.asarray(time_limits, dtype=np.float64)
+        self.stats.flush(range(B), eng)
+        eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=limits)
+        params = self.policy.packed_params(eng.device)
+        ctr = ((self.calls << 32) + 1 + self.row_offset * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        self.arena.clear()
+        steps = int(min(max_steps, 2**31 - 1))
+        while True:
+            eng.decima_rollout(params, self.seed, ctr, steps, samples=self.arena, num_tasks_scale=self.scales[0],
+                               work_scale=self.scales[1])
+            self.launches += 1
+            cur = self.arena.cursor.cpu().numpy()
+            if not (cur[:, _abi.CUR_FULL] != 0).any():
+                break
+            self.arena.grow(cur)
+        wall = eng.views["wall_time"].double().clone()
+        return self.arena.buffer(wall)
+
+
 class AsyncRolloutCollector(RolloutCollector):
     """RolloutWorkerAsync (rollout_worker.py:160-206): model updates at regular intervals of simulated time,
     regardless of episode boundaries. Each env (a "worker" row) keeps its episode across `collect` calls and

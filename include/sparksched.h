@@ -259,6 +259,49 @@ int ssim_decima_policy(ssim_handle* h, const float* node_feats, const int32_t* c
                        int32_t* job_idx, int32_t* exec_idx, float* lgprob, float* stage_scores, float* exec_scores,
                        int32_t* overflow, void* stream);
 
+/* ---- persistent Decima rollouts -------------------------------------------------
+ * One launch runs, per env and per decision: the Decima features of the current observation (as
+ * ssim_decima_features), the fused Decima policy (as ssim_decima_policy) and env.step with the sampled action, with
+ * no host round trip and no env waiting for another (replaces the per-decision loop of
+ * trainers/rollout_worker.py:135-157 RolloutWorkerSync.collect_rollout: DecimaObsWrapper.observation,
+ * DecimaScheduler.schedule, env.step). The optional sample arena receives what the PPO learner needs per decision
+ * (rollout_worker.py:18-46 RolloutBuffer: observation, action, log-probability, reward, wall time). */
+typedef struct ssim_decima_sample { /* 64 B, one per decision */
+  int32_t num_nodes, num_edges, num_dags, depth; /* observation sizes; depth as ssim_decima_features */
+  int32_t node_off, edge_off, dag_off;           /* first row of the observation in the env's node / edge / DAG region */
+  int32_t stage_idx, job_idx, exec_idx, num_exec;/* the action (as ssim_decima_policy's outputs) */
+  float lgprob;
+  double wall_before;                            /* wall time before the step */
+  double reward;                                 /* the step's reward */
+} ssim_decima_sample;
+typedef struct ssim_decima_samples {
+  int32_t* cursor;             /* device int32 [num_envs][8]: samples, node rows, edge rows, DAG rows used (the caller
+                                  zeroes it before a collection); [4] = 1 when the env stopped because a region was full
+                                  (grow the arena, clear the flag, launch again: the env continues where it stopped) */
+  ssim_decima_sample* rec;     /* [num_envs][cap_samples] */
+  float* nodes;                /* [num_envs][cap_nodes][6]: the 5 Decima node features, then the schedulable flag */
+  int32_t* edges;              /* [num_envs][cap_edges][4]: parent, child (node rows of the observation), edge-mask word, 0 */
+  int32_t* dags;               /* [num_envs][cap_dags][2]: node count, commit cap (exec_mask[j, :cap]) */
+  int32_t cap_samples, cap_nodes, cap_edges, cap_dags;
+} ssim_decima_samples;
+
+/* Bytes of the per-env workspace ssim_decima_rollout needs for this handle's layout (device memory, caller-owned). */
+int64_t ssim_decima_workspace_bytes(const ssim_handle* h);
+
+/* Decima rollouts in one launch. `params`/`num_params` as ssim_decima_policy; num_tasks_scale / work_scale as
+ * ssim_decima_features. Each env takes at most `max_steps` decisions. Sampling stream: (seed, env, counter + the env's
+ * decision index in its episode), plus (episode << 32) with SSIM_ROLLOUT_AUTORESET. flags:
+ *   0: collection — an env stops when its episode ends (terminated, truncated: wall_time >= its time limit);
+ *   SSIM_ROLLOUT_AUTORESET: finished episodes are reset in place (time_limits as ssim_rollout_ex) and the env goes on;
+ *   SSIM_ROLLOUT_PREEMPT with total_decisions > 0: a shared decision budget as ssim_rollout_budget;
+ *   SSIM_ROLLOUT_WARMUP: the launch runs under the symbol k_decima_rollout_warmup (unmeasured launches).
+ * total_decisions: 0 = no budget. samples: optional sample arena (NULL = none). action_log: optional int32
+ * [max_steps][num_envs][2] (stage_idx, num_exec of every decision started in this launch). */
+int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t num_params, float num_tasks_scale,
+                        float work_scale, uint64_t seed, uint64_t counter, int32_t max_steps, int64_t total_decisions,
+                        int32_t flags, const double* time_limits, void* workspace, int64_t workspace_bytes,
+                        const ssim_decima_samples* samples, int32_t* action_log, void* stream);
+
 const char* ssim_last_error(void);
 
 #ifdef __cplusplus

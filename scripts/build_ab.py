@@ -23,7 +23,8 @@ sys.path.insert(0, REPO)
 import __graft_entry__ as G  # noqa: E402
 
 AB = os.path.join(G.BUILD, "ab")
-VARIANT_TUS = ("sparksched.hip", "k_bench900.hip")
+# translation units recompiled per variant (AB_TUS, comma-separated; default: the ABI + the bench-shape kernels)
+VARIANT_TUS = tuple(os.environ.get("AB_TUS", "sparksched.hip,k_bench900.hip").split(","))
 
 
 def build_variant(name, defines):

@@ -49,6 +49,10 @@ for s in "$@"; do
     pmc_decima) step pmc_decima 900 env PMC_TAG=decima PMC_ARGS="--workload decima --steps 40 --warmup 5" bash scripts/pmc_profile.sh ;;
     ab20x)   step ab20x 1200 env AB_TAG=s20 AB_ARGS="--steps 20 --warmup 5" AB_REPS=3 bash scripts/ab_tpch.sh ;;
     prof_step) step prof_step 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_step" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step --steps 100 ;;
+    hostsim_rate) step hostsim_rate 300 python scripts/hostsim_rate.py 20 ;;
+    pmc_latency) step pmc_latency 600 env PMC_TAG=latency PMC_PASSES=latency bash scripts/pmc_profile.sh ;;
+    pmc_decima_persist) step pmc_decima_persist 900 env PMC_TAG=decima_persistent PMC_ARGS="--workload decima --steps 40 --warmup 5" bash scripts/pmc_profile.sh ;;
+    prof_decima_persist) step prof_decima_persist 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_decima_persist" -o run --output-format csv -- python3 bench.py --workload decima --steps 40 --warmup 5 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -666,7 +666,7 @@ def check_replayed_env(eng, v, ta, tc, i, o, ob, ep, dec, last, what, trace=Fals
 
 
 def case_bench_rollout_sequence(make, dataset, cfg, B, preroll, warmup, K, stride, mean_limit=None, trace_cap=0,
-                                seed=0, rank=0, expect_resident=None):
+                                seed=0, rank=0, expect_resident=None, policy="random"):
     """bench.py's rollout sequence verbatim (bench.py main(), rollout mode): the device reset with the rank's shard
     seeds and StochasticTimeLimit draws; the seeded pre-roll of U[0, preroll) decisions per env (ssim_rollout_steps,
     AUTORESET | WARMUP); one warm-up launch of `warmup` steps and the timed launch of K steps, both shared-budget
@@ -675,7 +675,9 @@ def case_bench_rollout_sequence(make, dataset, cfg, B, preroll, warmup, K, strid
     actions; each sampled env's actions, concatenated in launch order and replayed on the oracle with the same
     auto-resets (terminated, or truncated by the time limit), give its episode count, the decisions, wall time,
     job arrival / completion times and final observation of its current episode bit for bit (and, with trace_cap,
-    that episode's event trace). Reference: spark_sched_sim.py:127-343 (reset, step, the event loop)."""
+    that episode's event trace). Reference: spark_sched_sim.py:127-343 (reset, step, the event loop).
+    policy="decima": the budget launches are bench.py's configs[2] persistent Decima rollouts (ssim_decima_rollout:
+    features + fused GNN policy + step per env, random-init weights as bench.py), the pre-roll stays random."""
     from spark_sched_sim.distributed import shard_seeds
 
     SENT = -99
@@ -705,10 +707,24 @@ def case_bench_rollout_sequence(make, dataset, cfg, B, preroll, warmup, K, strid
     assert collect(log) == int(pre.sum())
     acc0 = np.array(eng.to_numpy(eng.views["acc"]), dtype=np.int64).copy()
     started = 0
+    if policy == "decima":
+        import torch
+
+        from spark_sched_sim.schedulers.decima import DecimaScheduler
+
+        torch.manual_seed(seed)
+        packed = DecimaScheduler(cfg["num_executors"]).to(eng.device).packed_params(eng.device)
+        dlim = None if lim is None else torch.tensor(lim, dtype=torch.float64, device=eng.device)
+
+        def budget_launch(c, f, log):
+            eng.decima_rollout(packed, seed, 1, 8 * c, B * c, flags=f, time_limits=dlim, action_log=log)
+    else:
+        def budget_launch(c, f, log):
+            eng.rollout_budget(kind, 1234, 8 * c, B * c, log, flags=f, time_limits=lim)
     for c, f in ((warmup, AR | PRE | WU), (K, AR | PRE)):
         log = eng.alloc_action_log(8 * c)
         log.fill_(SENT)
-        eng.rollout_budget(kind, 1234, 8 * c, B * c, log, flags=f, time_limits=lim)
+        budget_launch(c, f, log)
         n = collect(log)
         # the launch hands out its budget in chunks of <= 8 decisions; a wave stopped by preemption (or its step cap)
         # while holding part of a chunk leaves that part unstarted, so the steps started are within 8 per env of it

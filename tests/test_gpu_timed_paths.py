@@ -64,6 +64,23 @@ def test_bench_decima_env_deep_replay_hbm_rollout(make, dataset):
                                       mean_limit=2.0e7, expect_resident=False)
 
 
+def test_bench_decima_persistent_rollout_replay(make, dataset):
+    """configs[2] as bench.py --workload decima now times it: 4096 envs (J=200 / N=50, time limits), the pre-roll,
+    then the warm-up and timed persistent Decima rollouts (ssim_decima_rollout: features, fused GNN policy and step
+    per env in one launch, a shared budget, PREEMPT | AUTORESET) and a closing launch; every 512th env's actions
+    replayed on the oracle across its episode boundaries."""
+    r = cases.case_bench_rollout_sequence(make, dataset, DECIMA, B=4096, preroll=1500, warmup=5, K=20, stride=512,
+                                          mean_limit=2.0e7, expect_resident=False, policy="decima")
+    assert r["decisions_replayed"] > 8 * 700
+
+
+def test_decima_persistent_rollout_small_batch_replay(make, dataset):
+    """The LDS-resident instantiation of the persistent Decima rollout (batches of <= 256 J=200 envs, e.g. PPO's 16)
+    through the same budget sequence; every 4th env replayed on the oracle."""
+    cases.case_bench_rollout_sequence(make, dataset, DECIMA, B=16, preroll=300, warmup=5, K=40, stride=4,
+                                      mean_limit=2.0e6, expect_resident=True, policy="decima")
+
+
 @pytest.mark.parametrize("cfg,B,seed0", [(dict(DECIMA, beta=5e-3), 2, 11), (LARGE, 1, 21)])
 def test_forced_hbm_full_episode_lockstep(make, dataset, cfg, B, seed0):
     """J=200 full-episode lockstep cases that batches of <= 256 envs would run LDS-resident, forced onto the

@@ -370,3 +370,119 @@ def test_ppo_decima_tpch_iteration_gpu(gpu_device, dataset):
     after = torch.cat([p.detach().reshape(-1) for p in ppo.scheduler.parameters()])
     assert np.isfinite(info["policy loss"]) and info["samples"] == int(n.sum())
     assert not torch.equal(before, after)
+
+
+def _batch_equal(want, got, what):
+    for name in want.__dataclass_fields__:
+        a, b = getattr(want, name), getattr(got, name)
+        if isinstance(a, torch.Tensor):
+            assert a.dtype == b.dtype and a.shape == b.shape and torch.equal(a.cpu(), b.cpu()), f"{what}: {name}"
+        else:
+            assert a == b, f"{what}: {name}"
+
+
+def _fill_arena_like_kernel(arena, e, v, f):
+    """What csrc/decima_rollout.h DecimaPolicy.act writes for env e's current observation (host views v, host
+    features f): the node / edge / DAG rows after the env's cursor, and the record (action fields left 0)."""
+    from spark_sched_sim import _abi
+
+    c = v["counts"][e]
+    n, ne, nj = int(c[_abi.OC_NUM_NODES]), int(c[_abi.OC_NUM_EDGES]), int(c[_abi.OC_NUM_JOBS])
+    cur = arena.cursor[e]
+    cs, cn, ce, cg = (int(x) for x in cur[:4])
+    arena.nodes[e, cn:cn + n, :5] = torch.from_numpy(np.asarray(f["node_feats"][e, :n]))
+    arena.nodes[e, cn:cn + n, 5] = torch.from_numpy(np.asarray(v["nodes"][e, :n, 2]))
+    links = np.asarray(v["edge_links"][e, :ne], dtype=np.int64)
+    arena.edges[e, ce:ce + ne, 0] = torch.from_numpy(links[:, 0].astype(np.int32))
+    arena.edges[e, ce:ce + ne, 1] = torch.from_numpy(links[:, 1].astype(np.int32))
+    arena.edges[e, ce:ce + ne, 2] = torch.from_numpy(np.asarray(f["edge_mask"][e, :ne]).astype(np.int32))
+    ptr = np.asarray(v["dag_ptr"][e, : nj + 1], dtype=np.int64)
+    arena.dags[e, cg:cg + nj, 0] = torch.from_numpy((ptr[1:] - ptr[:-1]).astype(np.int32))
+    arena.dags[e, cg:cg + nj, 1] = torch.from_numpy(np.asarray(f["commit_cap"][e, :nj]).astype(np.int32))
+    rec = torch.zeros(16, dtype=torch.int32)
+    rec[:7] = torch.tensor([n, ne, nj, int(f["depth"][e]), cn, ce, cg], dtype=torch.int32)
+    arena.rec[e, cs] = rec
+    cur[:4] = torch.tensor([cs + 1, cn + n, ce + ne, cg + nj], dtype=torch.int32)
+
+
+def test_arena_buffer_matches_per_step_batches(dataset):
+    """The persistent Decima rollout's host side (trainers/rollouts.py ArenaRolloutBuffer.samples): a sample arena
+    filled the way the kernel fills it, from a host-engine rollout's observations and features, assembles into the
+    same DagBatch as the lockstep collector's per-step build_batch + cat_batches + row-major select_envs, every field
+    bit for bit; region growth keeps the used prefix."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.schedulers.decima import build_batch, cat_batches, select_envs
+    from spark_sched_sim.trainers.rollouts import DecimaSampleArena
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0)
+    B = 5
+    eng = _host_engine(cfg, B, dataset)
+    eng.reset(seeds=list(range(B)))
+    arena = DecimaSampleArena(B, "cpu", cap_samples=4, cap_nodes=64, cap_edges=64, cap_dags=8)
+    batches, envs = [], []
+    steps = [7, 0, 12, 3, 9]  # decisions per env (one env without any)
+    for k in range(max(steps)):
+        v = eng.host_views()
+        f = eng.decima_features_np()
+        live = [e for e in range(B) if k < steps[e]]
+        tv = {n: torch.from_numpy(np.asarray(x)) for n, x in v.items() if n != "trace"}
+        tf = {n: torch.from_numpy(np.asarray(x)) for n, x in f.items()}
+        batches.append(build_batch(tv, tf, envs=torch.tensor(live)))
+        envs.append(torch.tensor(live))
+        for e in live:
+            need = [int(arena.cursor[e, 0]) + 1, int(arena.cursor[e, 1]) + int(v["counts"][e][_abi.OC_NUM_NODES]),
+                    int(arena.cursor[e, 2]) + int(v["counts"][e][_abi.OC_NUM_EDGES]),
+                    int(arena.cursor[e, 3]) + int(v["counts"][e][_abi.OC_NUM_JOBS])]
+            while any(n > c for n, c in zip(need, arena.caps)):  # the kernel's full flag, then the host's growth
+                arena.cursor[e, _abi.CUR_FULL] = 1
+                arena.grow(arena.cursor.numpy())
+            _fill_arena_like_kernel(arena, e, v, f)
+        eng.rollout(_abi.SSIM_POLICY_RANDOM, 5, 1)
+    assert arena.caps[0] >= 12 and arena.caps[1] > 64  # grew
+    buf = arena.buffer(torch.zeros(B, dtype=torch.float64))
+    got, _ = buf.samples()
+    env = torch.cat(envs)
+    order = torch.argsort(env, stable=True)  # row-major (env, decision) order of the lockstep samples
+    want = select_envs(cat_batches(batches), order)
+    _batch_equal(want, got, "arena vs per-step batches")
+    _, _, lengths, sample = buf.trajectories()
+    assert lengths.tolist() == steps
+    assert torch.equal(sample[sample >= 0], torch.arange(sum(steps)))
+
+
+@pytest.mark.gpu
+def test_device_collector_matches_lockstep_gpu(gpu_device, dataset):
+    """The persistent collection (DeviceRolloutCollector: one ssim_decima_rollout launch) against the lockstep
+    fused collector (RolloutCollector: per decision features + policy + step launches) on the decima_tpch.yaml env
+    (J=200, N=50), 4 rows with StochasticTimeLimit draws: the same sampling stream, so the same actions; episode
+    lengths, wall times and rewards bit for bit, every observation of the gathered DagBatch bit for bit, log-probs
+    within float rounding."""
+    from spark_sched_sim.engine import DeviceEngine
+    from spark_sched_sim.schedulers.decima import DecimaScheduler, select_envs
+    from spark_sched_sim.trainers import DECIMA_TPCH
+    from spark_sched_sim.trainers.rollouts import DeviceRolloutCollector, RolloutCollector
+
+    env = {k: v for k, v in DECIMA_TPCH["env"].items() if k not in ("mean_time_limit", "dataset")}
+    B = 4
+    seeds = [101, 102, 103, 104]
+    limits = np.array([np.random.RandomState(s).exponential(3.0e6) for s in seeds])
+    torch.manual_seed(3)
+    pol = DecimaScheduler(env["num_executors"]).to(gpu_device)
+    bufs = []
+    for cls in (RolloutCollector, DeviceRolloutCollector):
+        eng = DeviceEngine(env, B, dataset, device=gpu_device)
+        col = cls(eng, pol, seed=77, row_offset=2)
+        bufs.append(col.collect(seeds, limits))
+    (t1, r1, l1, s1), (t2, r2, l2, s2) = (b.trajectories() for b in bufs)
+    assert torch.equal(l1, l2), (l1, l2)
+    assert int(l1.min()) > 50
+    assert torch.equal(t1, t2) and torch.equal(r1, r2)
+    o1, a1 = bufs[0].samples()
+    canon = s1[s1 >= 0]
+    o1 = select_envs(o1, canon)
+    a1 = {k: v[canon] for k, v in a1.items()}
+    o2, a2 = bufs[1].samples()
+    _batch_equal(o1, o2, "device vs lockstep observations")
+    for k in ("stage_idx", "job_idx", "exec_idx"):
+        assert torch.equal(a1[k].long(), a2[k].long()), k
+    assert torch.allclose(a1["lgprob"], a2["lgprob"], rtol=1e-5, atol=1e-5)
