@@ -5,8 +5,8 @@
 // (embed 16; GNN MLPs 5|16|21 -> 32 -> 16 -> 16 with LeakyReLU(0.2); policy MLPs 53|36 -> 64 -> 64 -> 1
 // with Tanh), reading the obs arena and the ssim_decima_features outputs directly. The batched PyTorch
 // module (spark_sched_sim/schedulers/decima.py) is the same math in ~150 small launches per decision; this
-// kernel is one launch, with every node's activations in LDS and the weights read through the scalar cache
-// (uniform addresses), each lane evaluating one node's (or edge's, DAG's, exec action's) MLP.
+// kernel is one launch, with every node's activations in the plan (LDS, or a global region) and the MLPs on the
+// matrix cores over tiles of 32 nodes / DAGs / exec actions (dp_mlp16, dp_mlp1).
 //
 // Semantics per env (matching DecimaScheduler.schedule):
 //   h_init = mlp_prep(x); without message-passing levels h = h_init (_forward_no_mp), else leaves
@@ -50,10 +50,11 @@ constexpr int kDecimaParams = kOffExec + MlpExec::kParams;  // 20802 (SURVEY.md 
 
 constexpr int64_t kDecimaPolicyLdsMax = 160 * 1024;  // gfx950 LDS per workgroup (opt-in above 64 KB)
 
-// LDS plan per env: h_init, h, agg [cap][16] f32, score f32 [cap], node->DAG i16 [cap], flags u8 [cap]
-// (bit0 has-child, bit1 level dst), h_dag [J][16] f32, glob [16] f32.
+// Plan per env: h_init, h, agg, msg [cap][16] f32, score f32 [cap], node->DAG i16 [cap], flags u8 [cap] (bit0
+// has-child), level marks u8 [cap] (bit0 child of a level edge, bit1 parent of one), compacted node lists i16 [cap]
+// (the level's children, the level's parents, the schedulable nodes), h_dag [J][16] f32, glob [16] f32.
 struct DpLds {
-  int64_t hi, hh, agg, score, ndag, flag, hdag, glob, total;
+  int64_t hi, hh, agg, msg, score, ndag, flag, mark, clist, plist, slist, hdag, glob, total;
 };
 __host__ __device__ inline DpLds dp_lds(int64_t cap, int64_t job_cap) {
   DpLds o{};
@@ -64,12 +65,22 @@ __host__ __device__ inline DpLds dp_lds(int64_t cap, int64_t job_cap) {
   b += cap * kDpEmb * 4;
   o.agg = b;
   b += cap * kDpEmb * 4;
+  o.msg = b;
+  b += cap * kDpEmb * 4;
   o.score = b;
   b += cap * 4;
   o.ndag = b;
   b = align16(b + cap * 2);
   o.flag = b;
   b = align16(b + cap);
+  o.mark = b;
+  b = align16(b + cap);
+  o.clist = b;
+  b = align16(b + cap * 2);
+  o.plist = b;
+  b = align16(b + cap * 2);
+  o.slist = b;
+  b = align16(b + cap * 2);
   o.hdag = b;  // one row per active job: a job with no active stage is complete, so #jobs <= #nodes <= cap
   b += (job_cap < cap ? job_cap : cap) * kDpEmb * 4;
   o.glob = b;
@@ -81,45 +92,124 @@ inline int64_t decima_policy_lds_bytes(int64_t node_cap, int64_t job_cap) { retu
 
 __device__ __forceinline__ float dp_leaky(float v) { return v >= 0.0f ? v : 0.2f * v; }
 
-// One lane's 3-layer MLP (act between layers, none after the last), weights via uniform addresses.
-// Packed layout per MLP (ssim_decima_policy): the FIRST layer's weight transposed ([IN][H1]) so the input loop
-// runs outermost over contiguous rows (each input is consumed once, only the H1 accumulators stay live);
-// layers 2 and 3 fused (each hidden-2 unit is activated and folded into the outputs at once, no H2 array).
-// Every sum runs in the same order as before (bias first, then ascending inputs), so the scores are
-// bit-identical to the unfused form.
-template <int IN, int H1, int H2, int OUT, bool kTanh>
-__device__ __forceinline__ void dp_mlp(const float* __restrict__ p, const float* in, float* out) {
-  const float* W0t = p;  // [IN][H1]
-  const float* b0 = W0t + H1 * IN;
+// MLPs on the matrix cores, one tile of 16 rows (nodes, DAGs or exec actions) per call: every layer is a transposed
+// product Y^T[units x 16 rows] = W[units x in] . X^T[in x 16 rows] + b on v_mfma_f32_16x16x4_f32 (f32 in, f32
+// accumulate: a k-ordered fmaf chain per output, no reduced precision). Lane l works on row l & 15; lane quarter
+// q = l >> 4 supplies input k = 4s + q of step s. The accumulator of a 16-unit tile holds, in register r of lane l,
+// unit 4q + r of row l & 15, and a hidden layer takes the previous layer's accumulators as its B operand (step r of
+// tile t' reads unit 16t' + 4q + r: the input order is permuted to match), so layers chain in registers. The weights
+// (ssim_decima_policy's layout: the module's parameters() in order, nn.Linear [out][in] weights) are gathered per
+// step as the A operand through one per-lane pointer per output tile (immediate step offsets). 16-row tiles fit the
+// observations of the Decima workloads (~16 nodes per decision at J=200); a per-lane MLP (one row per lane, weights
+// as scalar operands) left most lanes idle there and waited on a scalar load per weight row.
+typedef float dp_f32x4 __attribute__((ext_vector_type(4)));
+// Steps per scheduling group: a group's operand loads are issued together and not hoisted past the group before
+// (sched_barrier), which bounds the registers in flight.
+#ifndef SSIM_DP_GROUP
+#define SSIM_DP_GROUP 4
+#endif
+constexpr int kDpGroup = SSIM_DP_GROUP;
+
+template <bool kTanh>
+__device__ __forceinline__ float dp_act(float v) {
+  return kTanh ? tanhf(v) : dp_leaky(v);
+}
+
+// first layer: inputs xin(k), k < IN, of this lane's row (natural k order); W0 [H][IN] row-major (nn.Linear), b [H].
+// Each output tile's weight operand is read through one per-lane pointer with the step as an immediate offset.
+template <int IN, int H, class XF>
+__device__ __forceinline__ void dp_layer_in(const float* __restrict__ W0, const float* __restrict__ b, XF xin,
+                                            dp_f32x4 (&y)[H / 16]) {
+  static_assert(H % 16 == 0, "layer widths: multiples of 16");
+  constexpr int T = H / 16, STEPS = (IN + 3) / 4;
+  const int lane = (int)__lane_id(), q = lane >> 4, row = lane & 15;
+  const float* wl[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    wl[t] = W0 + (16 * t + row) * IN + q;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[t][r] = b[16 * t + 4 * q + r];
+  }
+#pragma unroll
+  for (int st = 0; st < STEPS; ++st) {
+    const bool kin = 4 * st + 3 < IN || 4 * st + q < IN;
+    const float xv = kin ? xin(4 * st + q) : 0.0f;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float wv = kin ? wl[t][4 * st] : 0.0f;
+      y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv, xv, y[t], 0, 0, 0);
+    }
+    if ((st & (kDpGroup - 1)) == kDpGroup - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+// hidden / output layer from the previous layer's accumulators x (HP units, activated here); Wm [H][HP] row-major
+template <int HP, int H, bool kTanh>
+__device__ __forceinline__ void dp_layer_h(const float* __restrict__ Wm, const float* __restrict__ b,
+                                           const dp_f32x4 (&x)[HP / 16], dp_f32x4 (&y)[H / 16]) {
+  static_assert(H % 16 == 0 && HP % 16 == 0, "layer widths: multiples of 16");
+  constexpr int T = H / 16, TP = HP / 16;
+  const int lane = (int)__lane_id(), q = lane >> 4, row = lane & 15;
+  const float* wl[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    wl[t] = Wm + (16 * t + row) * HP + 4 * q;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[t][r] = b[16 * t + 4 * q + r];
+  }
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float xv = dp_act<kTanh>(x[tp][r]);
+#pragma unroll
+      for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wl[t][16 * tp + r], xv, y[t], 0, 0, 0);
+      if (((4 * tp + r) & (kDpGroup - 1)) == kDpGroup - 1) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+// The weight pointer made opaque at each MLP call: every lane pointer and bias load derived from it is then
+// loop-variant, so the compiler does not hoist those of every MLP of the policy out of the tile loops to the function
+// entry (where they were all live at once: hundreds of VGPRs).
+__device__ __forceinline__ const float* dp_opaque(const float* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+// 3-layer MLP with 16 outputs (the GNN MLPs, LeakyReLU(0.2) between layers): y register r of lane l = output
+// 4 (l >> 4) + r of row l & 15
+template <int IN, int H1, int H2, class XF>
+__device__ __forceinline__ void dp_mlp16(const float* __restrict__ p0, XF xin, dp_f32x4 (&y)[1]) {
+  const float* p = dp_opaque(p0);
+  const float* W0 = p;  // [H1][IN]
+  const float* b0 = W0 + H1 * IN;
   const float* W1 = b0 + H1;  // [H2][H1]
   const float* b1 = W1 + H2 * H1;
-  const float* W2 = b1 + H2;  // [OUT][H2]
-  const float* b2 = W2 + OUT * H2;
-  float a[H1];
+  const float* W2 = b1 + H2;  // [16][H2]
+  const float* b2 = W2 + kDpEmb * H2;
+  dp_f32x4 a1[H1 / 16], a2[H2 / 16];
+  dp_layer_in<IN, H1>(W0, b0, xin, a1);
+  dp_layer_h<H1, H2, false>(W1, b1, a1, a2);
+  dp_layer_h<H2, kDpEmb, false>(W2, b2, a2, y);
+}
+// 3-layer MLP with one output (the policy score MLPs, Tanh between layers): the score of row l & 15, in every quarter
+template <int IN, int H1, int H2, class XF>
+__device__ __forceinline__ float dp_mlp1(const float* __restrict__ p0, XF xin) {
+  const float* p = dp_opaque(p0);
+  const float* W0 = p;  // [H1][IN]
+  const float* b0 = W0 + H1 * IN;
+  const float* W1 = b0 + H1;  // [H2][H1]
+  const float* b1 = W1 + H2 * H1;
+  const float* W2 = b1 + H2;  // [1][H2]
+  const float* b2 = W2 + H2;
+  dp_f32x4 a1[H1 / 16], a2[H2 / 16];
+  dp_layer_in<IN, H1>(W0, b0, xin, a1);
+  dp_layer_h<H1, H2, true>(W1, b1, a1, a2);
+  const int q = (int)__lane_id() >> 4;
+  float part = q == 0 ? b2[0] : 0.0f;  // the last layer (H2 -> 1) on the VALU: this quarter's units, then all four
 #pragma unroll
-  for (int j = 0; j < H1; ++j) a[j] = b0[j];
-#pragma unroll 1
-  for (int i = 0; i < IN; ++i) {
-    const float v = in[i];
+  for (int t = 0; t < H2 / 16; ++t)
 #pragma unroll
-    for (int j = 0; j < H1; ++j) a[j] = __builtin_fmaf(W0t[i * H1 + j], v, a[j]);
-  }
-#pragma unroll
-  for (int j = 0; j < H1; ++j) a[j] = kTanh ? tanhf(a[j]) : dp_leaky(a[j]);
-  float o[OUT];
-#pragma unroll
-  for (int k = 0; k < OUT; ++k) o[k] = b2[k];
-#pragma unroll 1
-  for (int j = 0; j < H2; ++j) {  // not unrolled: one weight row (H1 floats) in SGPRs at a time
-    float acc = b1[j];
-#pragma unroll
-    for (int i = 0; i < H1; ++i) acc = __builtin_fmaf(W1[j * H1 + i], a[i], acc);
-    const float c = kTanh ? tanhf(acc) : dp_leaky(acc);
-#pragma unroll
-    for (int k = 0; k < OUT; ++k) o[k] = __builtin_fmaf(W2[k * H2 + j], c, o[k]);
-  }
-#pragma unroll
-  for (int k = 0; k < OUT; ++k) out[k] = o[k];
+    for (int r = 0; r < 4; ++r) part = __builtin_fmaf(W2[16 * t + 4 * q + r], tanhf(a2[t][r]), part);
+  part += __shfl_xor(part, 16);
+  return part + __shfl_xor(part, 32);
 }
 
 // Gumbel(0,1) noise from a counter-based stream (splitmix64 of seed, env, counter, item).
@@ -173,8 +263,24 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
                                          const uint32_t* __restrict__ emask, const int32_t* __restrict__ depth,
                                          const float* __restrict__ Wt, int node_cap, uint64_t seed,
                                          uint64_t counter, int eid, uint8_t* lds, const DecimaPolicyOut& o,
-                                         DpAction* act = nullptr) {
+                                         DpAction* act = nullptr, uint64_t* prof = nullptr) {
   using W = WaveHip;
+  // diagnostic -DSSIM_PROFILE builds: shader cycles per part and the observation's sizes into prof[0..9] (LDS, lane 0)
+#ifdef SSIM_PROFILE
+  uint64_t tq = W::clock();
+  auto lap = [&](int slot) {
+    const uint64_t t = W::clock();
+    if (prof != nullptr && W::lane() == 0) W::lds_add_u64(prof + slot, t - tq);
+    tq = t;
+  };
+  auto count = [&](int slot, uint64_t v) {
+    if (prof != nullptr && W::lane() == 0) W::lds_add_u64(prof + slot, v);
+  };
+#else
+  (void)prof;
+  auto lap = [](int) {};
+  auto count = [](int, uint64_t) {};
+#endif
   const ssim_layout& L = P->L;
   const int S = L.stage_cap, J = L.job_cap, E = L.edge_cap, N = L.num_executors;
   const int32_t* cnt = reinterpret_cast<const int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
@@ -211,126 +317,185 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   float* hi = reinterpret_cast<float*>(lds + lo.hi);
   float* hh = reinterpret_cast<float*>(lds + lo.hh);
   float* agg = reinterpret_cast<float*>(lds + lo.agg);
+  float* msg = reinterpret_cast<float*>(lds + lo.msg);
   float* score = reinterpret_cast<float*>(lds + lo.score);
   int16_t* ndag = reinterpret_cast<int16_t*>(lds + lo.ndag);
   uint8_t* flag = lds + lo.flag;
+  uint8_t* mark = lds + lo.mark;
+  int16_t* clist = reinterpret_cast<int16_t*>(lds + lo.clist);
+  int16_t* plist = reinterpret_cast<int16_t*>(lds + lo.plist);
+  int16_t* slist = reinterpret_cast<int16_t*>(lds + lo.slist);
   float* hdag = reinterpret_cast<float*>(lds + lo.hdag);
   float* glob = reinterpret_cast<float*>(lds + lo.glob);
 
   // node -> DAG, flags
   for (int k = lane; k < nj; k += 64)
     for (int i = ptr[k]; i < ptr[k + 1]; ++i) ndag[i] = (int16_t)k;
-  for (int i = lane; i < n; i += 64) flag[i] = 0;
+  for (int i = lane; i < n; i += 64) {
+    flag[i] = 0;
+    mark[i] = 0;
+  }
   for (int k = lane; k < nj * kDpEmb; k += 64) hdag[k] = 0.0f;
   if (lane < kDpEmb) glob[lane] = 0.0f;
   scratch_sync<W, kGlobal>();
   for (int e = lane; e < ne; e += 64) flag[(int)links[2 * e]] = 1;  // parent has a child
   scratch_sync<W, kGlobal>();
-  // h_init = mlp_prep(x); h = h_init (no levels) or mlp_update(h_init) for leaves
-  for (int i = lane; i < n; i += 64) {
-    float xi[kDecimaFeatures], v[kDpEmb], u[kDpEmb];
+  lap(0);  // setup
+  count(5, (uint64_t)n);
+  count(6, (uint64_t)ne);
+  count(7, (uint64_t)levels);
+  // h_init = mlp_prep(x); h = h_init (no levels) or mlp_update(h_init) for leaves. Tiles of 16 nodes (every lane runs
+  // the matrix-core MLPs: the tile loops are wave-uniform); lane l stores outputs 4 (l >> 4) + r, r < 4, of node
+  // t0 + (l & 15).
+  const int hl = lane >> 4, rl = lane & 15;  // (matrix-core tiles: row, quarter)
+  for (int t0 = 0; t0 < n; t0 += 16) {
+    const int i = t0 + rl;
+    const bool ok = i < n;
+    dp_f32x4 v[1];
+    dp_mlp16<kDecimaFeatures, 32, 16>(Wt + kOffPrep, [&](int k) { return ok ? x[i * kDecimaFeatures + k] : 0.0f; }, v);
+    if (ok) {
 #pragma unroll
-    for (int f = 0; f < kDecimaFeatures; ++f) xi[f] = x[i * kDecimaFeatures + f];
-    dp_mlp<kDecimaFeatures, 32, 16, kDpEmb, false>(Wt + kOffPrep, xi, v);
-#pragma unroll
-    for (int f = 0; f < kDpEmb; ++f) hi[i * kDpEmb + f] = v[f];
+      for (int r = 0; r < 4; ++r) hi[i * kDpEmb + 4 * hl + r] = v[0][r];
+    }
     if (levels > 0) {
-      if (!(flag[i] & 1)) {
-        dp_mlp<kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffUpd, v, u);
+      scratch_sync<W, kGlobal>();
+      dp_f32x4 u[1];
+      dp_mlp16<kDpEmb, 32, 16>(Wt + kOffUpd, [&](int k) { return ok ? hi[i * kDpEmb + k] : 0.0f; }, u);
+      if (ok) {
+        const bool leaf = !(flag[i] & 1);
 #pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) hh[i * kDpEmb + f] = u[f];
-      } else {
-#pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) hh[i * kDpEmb + f] = 0.0f;
+        for (int r = 0; r < 4; ++r) hh[i * kDpEmb + 4 * hl + r] = leaf ? u[0][r] : 0.0f;
       }
-    } else {
+    } else if (ok) {
 #pragma unroll
-      for (int f = 0; f < kDpEmb; ++f) hh[i * kDpEmb + f] = v[f];
+      for (int r = 0; r < 4; ++r) hh[i * kDpEmb + 4 * hl + r] = v[0][r];
     }
   }
   scratch_sync<W, kGlobal>();
-  // message passing, deepest level first (reverse flow: children -> parents)
+  lap(1);  // prep
+  // message passing, deepest level first (reverse flow: children -> parents). Per level the MLPs run over compacted
+  // node lists (the level's children, then its parents): a lane-parallel pass over all edges or nodes would evaluate
+  // an MLP for every 64-row chunk holding ANY level row, i.e. nearly every chunk at every level. Each child's message
+  // is computed once (mlp_msg of its old h, as the reference's msg = mlp_msg(h) before the gather) and summed into
+  // every parent it reaches in the level.
   for (int lvl = levels - 1; lvl >= 0; --lvl) {
-    for (int e = lane; e < ne; e += 64) {  // zero agg and mark dst for the level's parents
-      if ((em[e] >> lvl) & 1u) {
-        const int p = (int)links[2 * e];
-#pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) agg[p * kDpEmb + f] = 0.0f;
-        flag[p] |= 2;
-      }
-    }
-    scratch_sync<W, kGlobal>();
-    for (int e = lane; e < ne; e += 64) {  // agg[p] += mlp_msg(h[c]) with the level's old h
+    for (int e = lane; e < ne; e += 64) {  // mark the level's children and parents, zero the parents' agg
       if ((em[e] >> lvl) & 1u) {
         const int p = (int)links[2 * e], c = (int)links[2 * e + 1];
-        float hc[kDpEmb], m[kDpEmb];
 #pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) hc[f] = hh[c * kDpEmb + f];
-        dp_mlp<kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffMsg, hc, m);
+        for (int f = 0; f < kDpEmb; ++f) agg[p * kDpEmb + f] = 0.0f;
+        mark[c] |= 1;  // (a node is only ever marked by lanes setting the same bit in one store: child and parent
+      }                //  marks go in separate passes below)
+    }
+    scratch_sync<W, kGlobal>();
+    for (int e = lane; e < ne; e += 64)
+      if ((em[e] >> lvl) & 1u) mark[(int)links[2 * e]] |= 2;
+    scratch_sync<W, kGlobal>();
+    int nc = 0, np = 0;  // compact (children, parents) in node order; clear the marks
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const int i = i0 + lane;
+      const int m = i < n ? mark[i] : 0;
+      const uint64_t bc = W::ballot(m & 1), bp = W::ballot(m & 2);
+      if (m & 1) clist[nc + W::rank(bc)] = (int16_t)i;
+      if (m & 2) plist[np + W::rank(bp)] = (int16_t)i;
+      if (m) mark[i] = 0;
+      nc += W::popc(bc);
+      np += W::popc(bp);
+    }
+    scratch_sync<W, kGlobal>();
+    for (int t0 = 0; t0 < nc; t0 += 16) {  // msg[c] = mlp_msg(h[c]) with the level's old h
+      const bool ok = t0 + rl < nc;
+      const int c = ok ? clist[t0 + rl] : 0;
+      dp_f32x4 m[1];
+      dp_mlp16<kDpEmb, 32, 16>(Wt + kOffMsg, [&](int k) { return ok ? hh[c * kDpEmb + k] : 0.0f; }, m);
+      if (ok) {
 #pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) dp_acc<kGlobal>(agg + p * kDpEmb + f, m[f]);
+        for (int r = 0; r < 4; ++r) msg[c * kDpEmb + 4 * hl + r] = m[0][r];
       }
     }
     scratch_sync<W, kGlobal>();
-    for (int i = lane; i < n; i += 64) {  // h[p] = h_init[p] + mlp_update(agg[p])
-      if (flag[i] & 2) {
-        float a[kDpEmb], u[kDpEmb];
+    for (int e = lane; e < ne; e += 64) {  // agg[p] += msg[c] over the level's edges
+      if ((em[e] >> lvl) & 1u) {
+        const int p = (int)links[2 * e], c = (int)links[2 * e + 1];
 #pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) a[f] = dp_ld<kGlobal>(agg + i * kDpEmb + f);
-        dp_mlp<kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffUpd, a, u);
+        for (int f = 0; f < kDpEmb; ++f) dp_acc<kGlobal>(agg + p * kDpEmb + f, msg[c * kDpEmb + f]);
+      }
+    }
+    scratch_sync<W, kGlobal>();
+    for (int t0 = 0; t0 < np; t0 += 16) {  // h[p] = h_init[p] + mlp_update(agg[p])
+      const bool ok = t0 + rl < np;
+      const int i = ok ? plist[t0 + rl] : 0;
+      dp_f32x4 u[1];
+      dp_mlp16<kDpEmb, 32, 16>(Wt + kOffUpd, [&](int k) { return ok ? dp_ld<kGlobal>(agg + i * kDpEmb + k) : 0.0f; },
+                               u);
+      if (ok) {
 #pragma unroll
-        for (int f = 0; f < kDpEmb; ++f) hh[i * kDpEmb + f] = hi[i * kDpEmb + f] + u[f];
-        flag[i] &= 1;
+        for (int r = 0; r < 4; ++r) {
+          const int f = 4 * hl + r;
+          hh[i * kDpEmb + f] = hi[i * kDpEmb + f] + u[0][r];
+        }
       }
     }
     scratch_sync<W, kGlobal>();
   }
+  lap(2);  // message passing
   // DAG and global summaries
-  for (int i = lane; i < n; i += 64) {
-    float in[kDecimaFeatures + kDpEmb], v[kDpEmb];
-#pragma unroll
-    for (int f = 0; f < kDecimaFeatures; ++f) in[f] = x[i * kDecimaFeatures + f];
-#pragma unroll
-    for (int f = 0; f < kDpEmb; ++f) in[kDecimaFeatures + f] = hh[i * kDpEmb + f];
-    dp_mlp<kDecimaFeatures + kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffDag, in, v);
-    const int g = ndag[i];
-#pragma unroll
-    for (int f = 0; f < kDpEmb; ++f) dp_acc<kGlobal>(hdag + g * kDpEmb + f, v[f]);
-  }
-  scratch_sync<W, kGlobal>();
-  for (int g = lane; g < nj; g += 64) {
-    float in[kDpEmb], v[kDpEmb];
-#pragma unroll
-    for (int f = 0; f < kDpEmb; ++f) in[f] = dp_ld<kGlobal>(hdag + g * kDpEmb + f);
-    dp_mlp<kDpEmb, 32, 16, kDpEmb, false>(Wt + kOffGlob, in, v);
-#pragma unroll
-    for (int f = 0; f < kDpEmb; ++f) dp_acc<kGlobal>(glob + f, v[f]);
-  }
-  scratch_sync<W, kGlobal>();
-  float gl[kDpEmb];
-#pragma unroll
-  for (int f = 0; f < kDpEmb; ++f) gl[f] = dp_ld<kGlobal>(glob + f);
-  // stage scores over schedulable nodes, then a categorical draw (max-shifted softmax, Gumbel-max)
-  const uint64_t key = splitmix64(seed ^ splitmix64((uint64_t)eid * 0x9E3779B97F4A7C15ULL + counter));
-  float mx = -__builtin_inff(), best = -__builtin_inff();
-  int pick = -1;
-  for (int i = lane; i < n; i += 64) {
-    if (nodes[3 * i + 2] != 0.0f) {
-      float in[kDecimaFeatures + 3 * kDpEmb], s;
+  for (int t0 = 0; t0 < n; t0 += 16) {
+    const int i = t0 + rl;
+    const bool ok = i < n;
+    dp_f32x4 v[1];
+    dp_mlp16<kDecimaFeatures + kDpEmb, 32, 16>(Wt + kOffDag, [&](int k) {
+      return !ok ? 0.0f : k < kDecimaFeatures ? x[i * kDecimaFeatures + k] : hh[i * kDpEmb + k - kDecimaFeatures];
+    }, v);
+    if (ok) {
       const int g = ndag[i];
 #pragma unroll
-      for (int f = 0; f < kDecimaFeatures; ++f) in[f] = x[i * kDecimaFeatures + f];
+      for (int r = 0; r < 4; ++r) dp_acc<kGlobal>(hdag + g * kDpEmb + 4 * hl + r, v[0][r]);
+    }
+  }
+  scratch_sync<W, kGlobal>();
+  for (int t0 = 0; t0 < nj; t0 += 16) {
+    const int g = t0 + rl;
+    const bool ok = g < nj;
+    dp_f32x4 v[1];
+    dp_mlp16<kDpEmb, 32, 16>(Wt + kOffGlob, [&](int k) { return ok ? dp_ld<kGlobal>(hdag + g * kDpEmb + k) : 0.0f; },
+                             v);
+    if (ok) {
 #pragma unroll
-      for (int f = 0; f < kDpEmb; ++f) {
-        in[kDecimaFeatures + f] = hh[i * kDpEmb + f];
-        in[kDecimaFeatures + kDpEmb + f] = dp_ld<kGlobal>(hdag + g * kDpEmb + f);
-        in[kDecimaFeatures + 2 * kDpEmb + f] = gl[f];
-      }
-      dp_mlp<kDecimaFeatures + 3 * kDpEmb, 64, 64, 1, true>(Wt + kOffStage, in, &s);
-      score[i] = s;
-      if (o.stage_scores) o.stage_scores[(int64_t)eid * S + i] = s;
-      mx = s > mx ? s : mx;
-      const float gs = s + dp_gumbel(key, (uint64_t)i);
+      for (int r = 0; r < 4; ++r) dp_acc<kGlobal>(glob + 4 * hl + r, v[0][r]);
+    }
+  }
+  scratch_sync<W, kGlobal>();
+  // stage scores over schedulable nodes, then a categorical draw (max-shifted softmax, Gumbel-max)
+  const uint64_t key = splitmix64(seed ^ splitmix64((uint64_t)eid * 0x9E3779B97F4A7C15ULL + counter));
+  lap(3);  // DAG / global summaries
+  int nsch = 0;  // the schedulable nodes, compacted in node order
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const bool sch = i < n && nodes[3 * i + 2] != 0.0f;
+    const uint64_t b = W::ballot(sch);
+    if (sch) slist[nsch + W::rank(b)] = (int16_t)i;
+    nsch += W::popc(b);
+  }
+  scratch_sync<W, kGlobal>();
+  float mx = -__builtin_inff(), best = -__builtin_inff();
+  int pick = -1;
+  for (int t0 = 0; t0 < nsch; t0 += 16) {  // score = mlp_stage([x, h, h_dag, h_glob]) per schedulable node
+    const bool ok = t0 + rl < nsch;
+    const int i = ok ? slist[t0 + rl] : 0;
+    const int g = ndag[i];
+    const float sc = dp_mlp1<kDecimaFeatures + 3 * kDpEmb, 64, 64>(Wt + kOffStage, [&](int k) {
+      return !ok                                   ? 0.0f
+             : k < kDecimaFeatures                 ? x[i * kDecimaFeatures + k]
+             : k < kDecimaFeatures + kDpEmb        ? hh[i * kDpEmb + k - kDecimaFeatures]
+             : k < kDecimaFeatures + 2 * kDpEmb    ? dp_ld<kGlobal>(hdag + g * kDpEmb + k - kDecimaFeatures - kDpEmb)
+                                                   : dp_ld<kGlobal>(glob + k - kDecimaFeatures - 2 * kDpEmb);
+    });
+    if (ok && hl == 0) {  // (every quarter holds the score; quarter 0 owns the row)
+      score[i] = sc;
+      if (o.stage_scores) o.stage_scores[(int64_t)eid * S + i] = sc;
+      mx = sc > mx ? sc : mx;
+      const float gs = sc + dp_gumbel(key, (uint64_t)i);
       if (gs > best) {
         best = gs;
         pick = i;
@@ -361,33 +526,34 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   }
   z = W::sum_f(z);
   const float lp_stage = score[node] - mx - logf(z);
+  lap(4);  // stage scores + draw
+  count(8, (uint64_t)nsch);
   // exec scores for k < commit cap of the chosen DAG
   const int g = ndag[node];
   const int cap = min(max(W::uni(cc[g]), 0), N);
-  float in[3 + 2 * kDpEmb + 1];
   const int p0 = ptr[g];
-#pragma unroll
-  for (int f = 0; f < 3; ++f) in[f] = x[p0 * kDecimaFeatures + f];
-#pragma unroll
-  for (int f = 0; f < kDpEmb; ++f) {
-    in[3 + f] = dp_ld<kGlobal>(hdag + g * kDpEmb + f);
-    in[3 + kDpEmb + f] = gl[f];
-  }
   float emx = -__builtin_inff(), ebest = -__builtin_inff(), es_k = 0.0f;
   int epick = -1;
   float* escore = agg;  // [N] (agg is free after message passing)
-  for (int k = lane; k < cap; k += 64) {  // exec action k/N per lane
-    float s;
-    in[3 + 2 * kDpEmb] = (float)k / (float)N;
-    dp_mlp<3 + 2 * kDpEmb + 1, 64, 64, 1, true>(Wt + kOffExec, in, &s);
-    escore[k] = s;
-    if (o.exec_scores) o.exec_scores[(int64_t)eid * N + k] = s;
-    emx = s > emx ? s : emx;
-    const float gs = s + dp_gumbel(key ^ 0xE7037ED1A0B428DBULL, (uint64_t)k);
-    if (gs > ebest) {
-      ebest = gs;
-      epick = k;
-      es_k = s;
+  for (int t0 = 0; t0 < cap; t0 += 16) {  // score of exec action k / N, k < cap, from [x_dag[:3], h_dag, h_glob, k/N]
+    const int k = t0 + rl;
+    const bool ok = k < cap;
+    const float sc = dp_mlp1<3 + 2 * kDpEmb + 1, 64, 64>(Wt + kOffExec, [&](int f) {
+      return f < 3             ? x[p0 * kDecimaFeatures + f]
+             : f < 3 + kDpEmb  ? dp_ld<kGlobal>(hdag + g * kDpEmb + f - 3)
+             : f < 3 + 2 * kDpEmb ? dp_ld<kGlobal>(glob + f - 3 - kDpEmb)
+                                  : (float)k / (float)N;
+    });
+    if (ok && hl == 0) {
+      escore[k] = sc;
+      if (o.exec_scores) o.exec_scores[(int64_t)eid * N + k] = sc;
+      emx = sc > emx ? sc : emx;
+      const float gs = sc + dp_gumbel(key ^ 0xE7037ED1A0B428DBULL, (uint64_t)k);
+      if (gs > ebest) {
+        ebest = gs;
+        epick = k;
+        es_k = sc;
+      }
     }
   }
   emx = W::max_f(emx);
@@ -405,6 +571,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     sk = __builtin_bit_cast(float, W::bcast_i(__builtin_bit_cast(int, es_k), l));
   }
   const float lp_exec = ew ? sk - emx - logf(ez) : 0.0f;
+  lap(9);  // exec scores + draw
   if (act != nullptr) *act = DpAction{rank, kx + 1, g, kx, lp_stage + lp_exec};
   if (lane == 0 && o.stage_idx != nullptr) {
     o.stage_idx[eid] = rank;

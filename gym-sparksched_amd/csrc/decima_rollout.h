@@ -83,6 +83,9 @@ struct DecimaPolicy {
         return false;
       }
     }
+#ifdef SSIM_PROFILE
+    uint64_t tp = W::clock();
+#endif
     uint8_t* wk = a.work + (int64_t)eid * a.wl.stride;
     float* feats = reinterpret_cast<float*>(a.work + a.wl.feats);
     int32_t* ccap = reinterpret_cast<int32_t*>(a.work + a.wl.ccap);
@@ -90,13 +93,26 @@ struct DecimaPolicy {
     int32_t* depth = reinterpret_cast<int32_t*>(a.work + a.wl.depth);
     DecimaView<W>{L, obs, eid}.template run<true>(a.num_tasks_scale, a.work_scale, wk + a.wl.feat_scratch, feats,
                                                   ccap, emask, depth);
+#ifdef SSIM_PROFILE
+    s.prof_add(kPhDecFeat, W::clock() - tp);
+    tp = W::clock();
+#endif
     const uint64_t ctr = a.counter + (uint64_t)s.h.decisions + (a.autoreset ? (uint64_t)s.h.episode << 32 : 0ull);
     DpAction act;
     const DecimaPolicyOut none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+#ifdef SSIM_PROFILE
+    uint64_t* pprof = s.prof + kPhDecParts;
+#else
+    uint64_t* pprof = nullptr;
+#endif
     decima_policy_env<true>(P, obs, feats, ccap, emask, depth, a.weights, L.stage_cap, a.seed, ctr, eid,
-                            wk + a.wl.plan, none, &act);
+                            wk + a.wl.plan, none, &act, pprof);
     out->stage_idx = act.stage_idx;
     out->num_exec = act.num_exec;
+#ifdef SSIM_PROFILE
+    s.prof_add(kPhDecPolicy, W::clock() - tp);
+    tp = W::clock();
+#endif
     if (sm.rec != nullptr) {  // the observation as the learner's DagBatch rows (schedulers/decima.py build_batch)
       const float* f = feats + (int64_t)eid * L.stage_cap * kDecimaFeatures;
       const float* nodes = reinterpret_cast<const float*>(obs + L.ob_nodes) + (int64_t)eid * L.stage_cap * 3;
@@ -148,6 +164,9 @@ struct DecimaPolicy {
       }
       W::sync();
     }
+#ifdef SSIM_PROFILE
+    s.prof_add(kPhDecRecord, W::clock() - tp);
+#endif
     return true;
   }
   // the decision's reward (observe() wrote it to the obs arena) into its sample
@@ -172,28 +191,28 @@ template <bool kRes>
 __device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                     DecimaRolloutArgs a, int num_steps, int flags,
                                                     const double* __restrict__ limits, uint8_t* reset,
-                                                    int32_t* action_log, int64_t budget) {
+                                                    int32_t* action_log, int64_t budget, uint64_t* prof_out) {
   a.autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   const DecimaPolicy pol{P, obs, a};
-  rollout_body<kRes, 0, 0, 0>(P, state, obs, pol, num_steps, flags, limits, reset, action_log, nullptr, budget,
+  rollout_body<kRes, 0, 0, 0>(P, state, obs, pol, num_steps, flags, limits, reset, action_log, prof_out, budget,
                               nullptr);
 }
 template <bool kRes>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_DECIMA_ROLLOUT_WAVES))) void k_decima_rollout(
     const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
-    const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget) {
-  decima_rollout_body<kRes>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget);
+    const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget, uint64_t* prof_out) {
+  decima_rollout_body<kRes>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
 }
 // launches that are not measured (SSIM_ROLLOUT_WARMUP), under their own symbol
 template <bool kRes>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_DECIMA_ROLLOUT_WAVES))) void k_decima_rollout_warmup(
     const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
-    const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget) {
-  decima_rollout_body<kRes>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget);
+    const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget, uint64_t* prof_out) {
+  decima_rollout_body<kRes>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
 }
 
 using DecimaRolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, DecimaRolloutArgs, int, int, const double*,
-                                 uint8_t*, int32_t*, int64_t);
+                                 uint8_t*, int32_t*, int64_t, uint64_t*);
 struct DecimaRolloutSet {
   DecimaRolloutFn rollout, rollout_warmup;
 };

@@ -75,7 +75,12 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
                  kHist0,
                  // s_memrealtime stamps (100 MHz chip clock): wave entry, hot block loaded, loop exit, hot block saved, engine
                  // constructed, fixed sections copied
-                 kTEntry = kHist0 + 16, kTLoaded, kTLoopEnd, kTSaved, kTCtor, kTCopy1, kNumPhases };
+                 kTEntry = kHist0 + 16, kTLoaded, kTLoopEnd, kTSaved, kTCtor, kTCopy1,
+                 // the persistent Decima rollout's action driver (decima_rollout.h): features, fused policy, sample copy
+                 kPhDecFeat, kPhDecPolicy, kPhDecRecord,
+                 // decima_policy_env's parts (setup, prep, message passing, summaries, stage scores, then sums of the
+                 // observation sizes n, ne, levels, schedulable, then exec scores)
+                 kPhDecParts, kNumPhases = kPhDecParts + 10 };
 #ifdef SSIM_PROFILE
 #define SSIM_COUNT(ph) prof_add(ph, 1)
 #else

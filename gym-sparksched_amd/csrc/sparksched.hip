@@ -59,13 +59,16 @@ __global__ __launch_bounds__(64) void k_decima(const Params* __restrict__ P, con
   v.run(nts, ws, g_smem, feats, ccap, emask, depth);
 }
 
+// `plan` null: the plan in LDS (dynamic shared memory); else a per-env region of global memory (stride plan_stride),
+// for node caps whose plan exceeds the LDS of a workgroup.
+template <bool kGlobal>
 __global__ __launch_bounds__(64) void k_decima_policy(const Params* __restrict__ P, const uint8_t* __restrict__ obs,
                                                       const float* __restrict__ feats, const int32_t* __restrict__ ccap,
                                                       const uint32_t* __restrict__ emask,
                                                       const int32_t* __restrict__ depth, const float* __restrict__ Wt,
                                                       int node_cap, uint64_t seed, uint64_t counter,
                                                       const uint8_t* __restrict__ env_mask, DecimaPolicyOut o,
-                                                      int32_t* overflow) {
+                                                      int32_t* overflow, uint8_t* plan, int64_t plan_stride) {
   const int eid = blockIdx.x;
   if (env_mask != nullptr && env_mask[eid] == 0) {
     if (WaveHip::lane() == 0) {
@@ -77,7 +80,8 @@ __global__ __launch_bounds__(64) void k_decima_policy(const Params* __restrict__
     }
     return;
   }
-  if (!decima_policy_env(P, obs, feats, ccap, emask, depth, Wt, node_cap, seed, counter, eid, g_smem, o) &&
+  uint8_t* lds = kGlobal ? plan + (int64_t)eid * plan_stride : g_smem;
+  if (!decima_policy_env<kGlobal>(P, obs, feats, ccap, emask, depth, Wt, node_cap, seed, counter, eid, lds, o) &&
       WaveHip::lane() == 0 && overflow != nullptr)
     atomicAdd(overflow, 1);
 }
@@ -120,6 +124,9 @@ struct ssim_handle {
   uint8_t* obs;
   uint8_t* reset;
   int ticket_slot;  // budget-launch decision counter in use next (k_rollout kFlagTicketSlot)
+  uint64_t* prof_next = nullptr;  // -DSSIM_PROFILE builds: per-wave phase sums of the next Decima rollout launch
+  uint8_t* policy_plan = nullptr;  // ssim_decima_policy's global plan when a node cap's plan exceeds the LDS
+  int64_t policy_plan_bytes = 0;
 };
 
 static thread_local char g_err[512] = "";
@@ -221,6 +228,7 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
 }
 
 extern "C" int ssim_destroy(ssim_handle* h) {
+  if (h != nullptr && h->policy_plan != nullptr) (void)hipFree(h->policy_plan);
   delete h;
   return SSIM_OK;
 }
@@ -352,6 +360,14 @@ extern "C" int ssim_rollout_budget_profiled(ssim_handle* h, int32_t kind, uint64
 }
 #endif
 
+#ifdef SSIM_PROFILE
+// Diagnostic build only: the next ssim_decima_rollout launch on `h` writes its per-wave phase sums to prof_out.
+extern "C" int ssim_decima_profile_next(ssim_handle* h, uint64_t* prof_out) {
+  h->prof_next = prof_out;
+  return SSIM_OK;
+}
+#endif
+
 extern "C" int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_completed, int32_t* state, void* stream) {
   if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_job_times: null handle");
   hipLaunchKernelGGL(k_job_times, dim3(h->params.L.num_envs), dim3(64), 0, (hipStream_t)stream, dparams(h), h->state,
@@ -393,9 +409,26 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
   if (node_cap <= 0 || node_cap > L.stage_cap) node_cap = L.stage_cap;
   if (node_cap < (L.num_executors + kDpEmb - 1) / kDpEmb) node_cap = (L.num_executors + kDpEmb - 1) / kDpEmb;
   const int64_t lds = decima_policy_lds_bytes(node_cap, L.job_cap);
-  if (lds > kDecimaPolicyLdsMax)
-    return set_err(SSIM_E_ARG, "ssim_decima_policy: node_cap %d needs %lld B of LDS (max %lld)", node_cap,
-                   (long long)lds, (long long)kDecimaPolicyLdsMax);
+  DecimaPolicyOut o{stage_idx, num_exec, job_idx, exec_idx, lgprob, stage_scores, exec_scores};
+  if (lds > kDecimaPolicyLdsMax) {  // the plan in a handle-owned global region (grown on demand)
+    const int64_t stride = (lds + 255) & ~int64_t(255), need = stride * L.num_envs;
+    if (need > h->policy_plan_bytes) {
+      if (h->policy_plan != nullptr) {
+        int rc = hip_check(hipStreamSynchronize((hipStream_t)stream), "policy plan resize sync");
+        if (rc != SSIM_OK) return rc;
+        (void)hipFree(h->policy_plan);
+        h->policy_plan = nullptr;
+        h->policy_plan_bytes = 0;
+      }
+      int rc = hip_check(hipMalloc(&h->policy_plan, (size_t)need), "policy plan allocation");
+      if (rc != SSIM_OK) return rc;
+      h->policy_plan_bytes = need;
+    }
+    hipLaunchKernelGGL(k_decima_policy<true>, dim3(L.num_envs), dim3(64), 0, (hipStream_t)stream, dparams(h), h->obs,
+                       node_feats, commit_cap, edge_mask, depth, params, node_cap, seed, counter, env_mask, o, overflow,
+                       h->policy_plan, stride);
+    return hip_check(hipGetLastError(), "k_decima_policy(global plan) launch");
+  }
   if (lds > 64 * 1024) {
     // hipFuncSetAttribute is per-device state: remember the raised limit per device (a process may drive
     // several GPUs); the cache is a fast path only, a race at worst repeats the (idempotent) call
@@ -404,16 +437,16 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
     int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
     if (rc != SSIM_OK) return rc;
     if (dev < 0 || dev >= 64 || lds > configured[dev]) {
-      rc = hip_check(hipFuncSetAttribute((const void*)k_decima_policy, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)lds), "k_decima_policy LDS attribute");
+      rc = hip_check(hipFuncSetAttribute((const void*)k_decima_policy<false>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                     "k_decima_policy LDS attribute");
       if (rc != SSIM_OK) return rc;
       if (dev >= 0 && dev < 64) configured[dev] = lds;
     }
   }
-  DecimaPolicyOut o{stage_idx, num_exec, job_idx, exec_idx, lgprob, stage_scores, exec_scores};
-  hipLaunchKernelGGL(k_decima_policy, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream, dparams(h),
-                     h->obs, node_feats, commit_cap, edge_mask, depth, params, node_cap, seed, counter, env_mask, o,
-                     overflow);
+  hipLaunchKernelGGL(k_decima_policy<false>, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream,
+                     dparams(h), h->obs, node_feats, commit_cap, edge_mask, depth, params, node_cap, seed, counter,
+                     env_mask, o, overflow, (uint8_t*)nullptr, (int64_t)0);
   return hip_check(hipGetLastError(), "k_decima_policy launch");
 }
 
@@ -469,7 +502,9 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
   if (rc != SSIM_OK) return rc;
   if (total_decisions > 0 && h->ticket_slot) flags |= kFlagTicketSlot;
   hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream, dparams(h),
-                     h->state, h->obs, a, max_steps, flags, time_limits, h->reset, action_log, total_decisions);
+                     h->state, h->obs, a, max_steps, flags, time_limits, h->reset, action_log, total_decisions,
+                     h->prof_next);
+  h->prof_next = nullptr;
   const int rc2 = hip_check(hipGetLastError(), "k_decima_rollout launch");
   if (rc2 == SSIM_OK && total_decisions > 0) h->ticket_slot ^= 1;
   return rc2;

@@ -330,6 +330,28 @@ class NodeEncoder(nn.Module):
         parent, child = b.edge_index[0], b.edge_index[1]
         ones = torch.ones(parent.numel(), dtype=h_init.dtype, device=h_init.device)
         has_child = torch.zeros(Nt, dtype=h_init.dtype, device=h_init.device).index_add_(0, parent, ones) > 0
+        if per_obs_no_mp:  # schedule (rollouts): the dense form, whose per-row results do not depend on the batch
+            return self._dense(b, h_init, has_child, parent, child)
+        # evaluate_actions (the learner): the MLPs run on the rows that need them only (leaves; per level its edges'
+        # children and its parents). A learner batch of J=200 observations holds millions of node rows and up to ~18
+        # levels, and an MLP over every row at every level was most of the learner's time. Same values as the dense
+        # form up to the GEMM shapes (the reference's masked sparse matmul sums the level's child messages into their
+        # parents); rollouts keep the dense form so a row's actions and log-probs do not depend on which other rows
+        # share its batch (the multi-rank learner's bit-equality with one rank).
+        leaves = torch.nonzero(~has_child).squeeze(1)
+        h = torch.zeros_like(h_init).index_put((leaves,), self.mlp_update(h_init[leaves]))
+        for lvl in range(b.max_levels - 1, -1, -1):
+            eidx = torch.nonzero((b.edge_bits >> lvl) & 1).squeeze(1)
+            if eidx.numel() == 0:
+                continue
+            p, c = parent[eidx], child[eidx]
+            agg = torch.zeros_like(h).index_add_(0, p, self.mlp_msg(h[c]))
+            dst = torch.unique(p)
+            h = h.index_put((dst,), h_init[dst] + self.mlp_update(agg[dst]))
+        return h
+
+    def _dense(self, b: DagBatch, h_init, has_child, parent, child) -> torch.Tensor:
+        Nt = h_init.shape[0]
         h = torch.where(has_child[:, None], torch.zeros_like(h_init), self.mlp_update(h_init))
         for lvl in range(b.max_levels - 1, -1, -1):
             w = ((b.edge_bits >> lvl) & 1).to(h.dtype)
@@ -337,10 +359,9 @@ class NodeEncoder(nn.Module):
             agg = torch.zeros_like(h).index_add_(0, parent, msg[child] * w[:, None])
             dst = torch.zeros(Nt, dtype=h.dtype, device=h.device).index_add_(0, parent, w) > 0
             h = torch.where(dst[:, None], h_init + self.mlp_update(agg), h)
-        if per_obs_no_mp:  # observations without message-passing levels keep h = mlp_prep(x)
-            flat = (b.env_levels == 0)[b.node_env]
-            h = torch.where(flat[:, None], h_init, h)
-        return h
+        # schedule's convention: observations without message-passing levels keep h = mlp_prep(x)
+        flat = (b.env_levels == 0)[b.node_env]
+        return torch.where(flat[:, None], h_init, h)
 
 
 class DagEncoder(nn.Module):
@@ -388,10 +409,16 @@ class StagePolicyNetwork(nn.Module):
         self.mlp_score = make_mlp(num_node_features + emb_dims["node"] + emb_dims["dag"] + emb_dims["glob"],
                                   output_dim=1, **mlp_kwargs)
 
-    def scores_all(self, b: DagBatch, h: dict[str, torch.Tensor]) -> torch.Tensor:
-        """Score of every node row (only schedulable rows are meaningful)."""
-        inp = torch.cat([b.x, h["node"], h["dag"][b.node_dag], h["glob"][b.node_env]], dim=1)
-        return self.mlp_score(inp).squeeze(-1)
+    def scores_all(self, b: DagBatch, h: dict[str, torch.Tensor], compact: bool = False) -> torch.Tensor:
+        """Score of every node row (only schedulable rows are meaningful). compact (the learner): the MLP runs on the
+        schedulable rows only, the others are 0."""
+        if not compact:
+            inp = torch.cat([b.x, h["node"], h["dag"][b.node_dag], h["glob"][b.node_env]], dim=1)
+            return self.mlp_score(inp).squeeze(-1)
+        idx = torch.nonzero(b.stage_mask).squeeze(1)
+        inp = torch.cat([b.x[idx], h["node"][idx], h["dag"][b.node_dag[idx]], h["glob"][b.node_env[idx]]], dim=1)
+        out = torch.zeros(b.x.shape[0], dtype=h["node"].dtype, device=b.x.device)
+        return out.index_put((idx,), self.mlp_score(inp).squeeze(-1))
 
     def forward(self, b: DagBatch, h: dict[str, torch.Tensor]) -> torch.Tensor:
         """The reference's output: one score per schedulable node, in flat node order."""
@@ -508,10 +535,9 @@ class DecimaScheduler(nn.Module):
 
     @torch.no_grad()
     def packed_params(self, dev) -> torch.Tensor:
-        """fp32 parameters in parameters() order for ssim_decima_policy, each MLP's first-layer weight
-        transposed to [in][out] (the kernel's input-outer loop reads contiguous rows)."""
-        return torch.cat([(p.detach().t() if n.endswith(".0.weight") else p.detach()).reshape(-1).float()
-                          for n, p in self.named_parameters()]).to(dev).contiguous()
+        """fp32 parameters in parameters() order (nn.Linear [out][in] weights) for ssim_decima_policy /
+        ssim_decima_rollout, as one contiguous device buffer."""
+        return torch.cat([p.detach().reshape(-1).float() for p in self.parameters()]).to(dev).contiguous()
 
     @torch.no_grad()
     def schedule_fused(self, engine, feats: dict | None = None, seed: int = 0, counter: int = 0,
@@ -565,7 +591,7 @@ class DecimaScheduler(nn.Module):
         B = b.num_envs
         dev = b.x.device
         h = self.encoder(b, per_obs_no_mp=False)
-        scores = self.stage_policy_network.scores_all(b, h)
+        scores = self.stage_policy_network.scores_all(b, h, compact=True)
         probs, logp = masked_softmax_stats(scores, b.stage_mask, b.node_env, B, clamp=True)
         rows = torch.arange(b.x.shape[0], device=dev)
         hit = b.stage_mask & (self._sched_rows(b) == stage_idx.long()[b.node_env])

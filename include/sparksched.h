@@ -246,10 +246,10 @@ int ssim_decima_features(ssim_handle* h, float num_tasks_scale, float work_scale
  * num_params must be 20802): one launch encodes every env's DAG batch from the obs arena and the
  * ssim_decima_features outputs, scores the schedulable stages and the exec actions, and samples both
  * (Gumbel-max on a counter-based stream of (seed, env, counter)). `params`: fp32 device buffer, the
- * module's parameters in DecimaScheduler.parameters() order, torch nn.Linear layout except that each MLP's
- * first-layer weight is transposed to [in][out] (DecimaScheduler.packed_params). `node_cap`: LDS
- * plan (>= the largest env's node count; 0 = stage_cap); envs above it are skipped and counted in
- * `overflow` (device int32, optional). env_mask (optional uint8 [B]): 0 = skip the env.
+ * module's parameters in DecimaScheduler.parameters() order, torch nn.Linear layout (DecimaScheduler.packed_params). `node_cap`: the per-env
+ * activation plan (>= the largest env's node count; 0 = stage_cap); envs above it are skipped and counted in
+ * `overflow` (device int32, optional). The plan lives in LDS when it fits a workgroup's 160 KB, else in a global
+ * region the handle allocates (and grows) on demand. env_mask (optional uint8 [B]): 0 = skip the env.
  * Outputs [B]: stage_idx (index among schedulable stages, -1 none), num_exec (= 1 + exec_idx), job_idx
  * (active-job index), exec_idx, lgprob (log-probability of both choices); optional stage_scores
  * [B][stage_cap] and exec_scores [B][N] (for checking). */

@@ -53,6 +53,7 @@ for s in "$@"; do
     pmc_latency) step pmc_latency 600 env PMC_TAG=latency PMC_PASSES=latency bash scripts/pmc_profile.sh ;;
     pmc_decima_persist) step pmc_decima_persist 900 env PMC_TAG=decima_persistent PMC_ARGS="--workload decima --steps 40 --warmup 5" bash scripts/pmc_profile.sh ;;
     prof_decima_persist) step prof_decima_persist 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_decima_persist" -o run --output-format csv -- python3 bench.py --workload decima --steps 40 --warmup 5 --no-cpu-baseline ;;
+    phase_decima) step phase_decima 600 python scripts/phase_profile_decima.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -22,6 +22,10 @@ PHASES = ["policy", "action", "round_check", "fulfill", "pop", "handle", "post_s
           f"#decisions {1 << (b + 10)}-{1 << (b + 11)} cycles" for b in range(16)]
 TOP = 8  # the first TOP phases are disjoint; the rest are inclusive sub-timers
 NSTAMPS = 6  # engine.h kTEntry, kTLoaded, kTLoopEnd, kTSaved, kTCtor, kTCopy1
+DEC_PHASES = ["(decima features)", "(decima policy)", "(decima sample copy)"]  # engine.h kPhDecFeat.. (inside policy)
+DEC_PARTS = ["[policy setup]", "[policy prep MLPs]", "[policy message passing]", "[policy DAG/global summaries]",
+             "[policy stage scores]", "#nodes", "#edges", "#levels", "#schedulable", "[policy exec scores]"]
+NUM_SLOTS = 40 + NSTAMPS + len(DEC_PHASES) + len(DEC_PARTS)  # engine.h kNumPhases
 
 
 def build_prof():
@@ -68,7 +72,7 @@ def main():
         acc = eng.views["acc"]
         d0 = acc[:, _abi.ACC_DECISIONS].sum().item()
         e0 = acc[:, 3].sum().item()
-        prof = torch.zeros((B, len(PHASES) + NSTAMPS), dtype=torch.int64, device=eng.device)
+        prof = torch.zeros((B, NUM_SLOTS), dtype=torch.int64, device=eng.device)
         rc = lib.ssim_rollout_budget_profiled(eng.handle, _abi.SSIM_POLICY_RANDOM, 1234, 8 * K, B * K, flags,
                                               prof.data_ptr(), eng._stream())
         native.check(rc, "ssim_rollout_budget_profiled")
@@ -76,7 +80,7 @@ def main():
         d1 = acc[:, _abi.ACC_DECISIONS].sum().item()
         e1 = acc[:, 3].sum().item()
         p = prof[:, :len(PHASES)].cpu().numpy().astype(np.float64)  # s_memtime ticks = shader cycles
-        st = prof[:, len(PHASES):].cpu().numpy().astype(np.float64)  # 100 MHz stamps
+        st = prof[:, len(PHASES):len(PHASES) + NSTAMPS].cpu().numpy().astype(np.float64)  # 100 MHz stamps
         eng.close()
         dec = d1 - d0
         tot = p.sum(axis=0)
