@@ -80,7 +80,9 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
                  kPhDecFeat, kPhDecPolicy, kPhDecRecord,
                  // decima_policy_env's parts (setup, prep, message passing, summaries, stage scores, then sums of the
                  // observation sizes n, ne, levels, schedulable, then exec scores)
-                 kPhDecParts, kNumPhases = kPhDecParts + 10 };
+                 kPhDecParts,
+                 // in-launch auto-resets (rollout_body): cycles, count
+                 kPhReset = kPhDecParts + 10, kCtReset, kNumPhases };
 #ifdef SSIM_PROFILE
 #define SSIM_COUNT(ph) prof_add(ph, 1)
 #else
@@ -128,7 +130,8 @@ struct HotParams {
   double moving_delay, warmup_delay, beta, job_arrival_gap;
   int64_t ob_nodes, ob_edge_links, ob_dag_ptr, ob_supplies, ob_frontier, ob_sched_rank, ob_counts, ob_reward,
       ob_wall_time, ob_acc, ob_trace;
-  int32_t num_templates, trace_cap, edge_cap, job_arrival_cap, topo, pad;
+  int32_t num_templates, trace_cap, edge_cap, job_arrival_cap, topo;
+  int32_t dcache;  // 1: every duration list fits the packed descriptor cache (len <= 255, offset < 2^24)
 };
 static_assert(sizeof(HotParams) <= 256 && sizeof(HotParams) % 8 == 0, "one dword per lane of one VGPR");
 
@@ -215,7 +218,7 @@ inline void fill_hot_params(Params* p) {
   h.edge_cap = L.edge_cap;
   h.job_arrival_cap = p->C.job_arrival_cap;
   h.topo = (p->C.max_stages <= 32 && D.ts_topo != nullptr) ? 1 : 0;
-  h.pad = 0;
+  h.dcache = 0;  // set by the host once it has checked the dataset's descriptors (dcache_fits)
 }
 
 // kN / kJ / kS: executor count, job cap and stage cap as compile-time constants (0 = read from the layout at
@@ -267,6 +270,8 @@ struct Sim {
   // task start (run_next_task) and for the pending tasks when a launch starts (ev_regs_load). (Kept in LDS: as a
   // register array in the Sim object it pushed the whole object into scratch memory.)
   static constexpr bool kDurCache = W::kWidth == 64 && kN > 0 && kN <= kDurCacheMaxExecs && SSIM_DUR_CACHE;
+  bool dcache_on = false;  // kDurCache and the dataset's descriptors fit the packed form (HotParams::dcache)
+  __device__ __forceinline__ bool dc_on() const { return kDurCache && dcache_on; }
   const HotParams* HPp;  // host build: Params::hp read in place
   uint32_t hpv;          // device: dword `lane` of Params::hp
 #ifdef SSIM_PROFILE
@@ -291,6 +296,7 @@ struct Sim {
         cold(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes + O.hot_bytes),
         scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index) {
     iv_lane = W::lane() < kIvRows ? *reinterpret_cast<const uint32_t*>(IV[W::lane()]) : 0u;
+    dcache_on = kDurCache && W::uni(p->hp.dcache) != 0;
     HPp = &p->hp;
     hpv = (W::kWidth == 64 && W::lane() < (int)(sizeof(HotParams) / 4)) ? reinterpret_cast<const uint32_t*>(&p->hp)[W::lane()]
                                                                       : 0u;
@@ -1070,7 +1076,7 @@ struct Sim {
         evr[p].ts = ((int32_t)r.ev_type << 16) | (uint16_t)r.ev_stage;
       }
     }
-    if constexpr (kDurCache) {  // the pending tasks' descriptors (independent gathers, one latency)
+    if (dc_on()) {  // the pending tasks' descriptors (independent gathers, one latency)
       for (int e = 0; e < kN; ++e) {
         const ExecRec x = ld_rec(exr(e));
         const bool task = x.ev_seq >= 0 && x.ev_type == kEvTask && x.ev_stage >= 0;
@@ -1142,18 +1148,17 @@ struct Sim {
   struct DurDesc {
     int len, off;  // this lane's descriptor (device) — unused by a 1-lane build
   };
-  struct alignas(8) DescPair {
-    int32_t len, off;
-  };
+  // packed: offset << 8 | length (a missing list, length -1, stores 0: both mean "no draw")
   __device__ __forceinline__ void dcache_store(int e, const DurDesc& d) {
-    if (W::lane() < 24) S<DescPair>(O.sc_dcache)[e * 24 + W::lane()] = DescPair{d.len, d.off};
+    if (W::lane() < 24)
+      S<uint32_t>(O.sc_dcache)[e * 24 + W::lane()] = d.len > 0 ? ((uint32_t)d.off << 8) | (uint32_t)d.len : 0u;
   }
   __device__ __forceinline__ DurDesc dcache_load(int e) const {
     DurDesc d{0, 0};
     if (W::lane() < 24) {
-      const DescPair v = S<DescPair>(O.sc_dcache)[e * 24 + W::lane()];
-      d.len = v.len;
-      d.off = v.off;
+      const uint32_t v = S<uint32_t>(O.sc_dcache)[e * 24 + W::lane()];
+      d.len = (int)(v & 0xFFu);
+      d.off = (int)(v >> 8);
     }
     return d;
   }
@@ -1371,7 +1376,7 @@ struct Sim {
     StageRec s = ld_rec(sraw);
     ExecRec x = ld_rec(xraw);
     const DurDesc dd = dur_gather(s.ts);
-    if constexpr (kDurCache) dcache_store(e, dd);
+    if (dc_on()) dcache_store(e, dd);
     run_next_task_rec(e, g, s, x, dd);
     stage(g) = s;
     exr(e) = x;
@@ -1746,11 +1751,9 @@ struct Sim {
           const StageRec sraw = stage(g);
           const ExecRec xraw = exr(e);
           DurDesc ddc{0, 0};
-          if constexpr (kDurCache) ddc = dcache_load(e);
+          if (dc_on()) ddc = dcache_load(e);
           const StageRec sr = ld_rec(sraw);
-          if constexpr (!kDurCache) {
-            if (sr.rem > 0) ddc = dur_gather(sr.ts);
-          }
+          if (!dc_on() && sr.rem > 0) ddc = dur_gather(sr.ts);
           // the next task's duration descriptors (if the stage has tasks left): issued now, used after the job
           // record read
           on_task_done(e, g, sr, ld_rec(xraw), ddc);

@@ -161,8 +161,15 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
     if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit) &&
         !s.pending()) {  // (a step preempted past the time limit completes first)
       if (stop.on && granted == 0 && (granted = stop.claim(B, last)) == 0) break;
+#ifdef SSIM_PROFILE
+      const uint64_t tr = WaveHip::clock();
+#endif
       s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
                       reset + (int64_t)eid * P->L.reset_stride);
+#ifdef SSIM_PROFILE
+      s.prof_add(kPhReset, WaveHip::clock() - tr);
+      s.prof_add(kCtReset, 1);
+#endif
       continue;
     }
     double st0 = 0.0;

@@ -142,7 +142,7 @@ struct StateOffsets {
       sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/;
   int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
-      sc_row_of /*int16[S]*/, sc_dcache /*int32x2[N][24] when N <= kDurCacheMaxExecs*/,
+      sc_row_of /*int16[S]*/, sc_dcache /*uint32[N][24] when N <= kDurCacheMaxExecs*/,
       sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build only*/;
 };
 
@@ -214,7 +214,7 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   O.sc_row_of = s;
   s = align16(s + 2 * S);
   O.sc_dcache = s;  // engine.h duration-descriptor cache (kernels specialised on few executors)
-  s = align16(s + (N <= kDurCacheMaxExecs ? 8 * 24 * N : 0));
+  s = align16(s + (N <= kDurCacheMaxExecs ? 4 * 24 * N : 0));
   O.sc_prof = s;
 #ifdef SSIM_PROFILE
   s += 8 * 64;
@@ -254,6 +254,7 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
                         ? 1 : 0;
   L->lds_resident = O->lds_resident;
   O->lds_bytes = O->scratch_bytes + (O->lds_resident ? O->hot_bytes : 0);
+  L->lds_bytes = O->lds_bytes;
 
   // obs arena: each field is [B][per-env]
   int64_t b = 0;

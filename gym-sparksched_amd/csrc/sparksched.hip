@@ -212,6 +212,25 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
       return rc0;
     }
   }
+  {  // the duration-descriptor cache (engine.h) packs offset << 8 | length: usable when every list fits
+    const int64_t nd = (int64_t)dataset->num_template_stages * 3 * kNumLevels;
+    int32_t* dl = new int32_t[nd > 0 ? nd : 1];
+    int32_t* dof = new int32_t[nd > 0 ? nd : 1];
+    int rc0 = nd <= 0 ? SSIM_OK : hip_check(hipMemcpy(dl, dataset->dur_len, sizeof(int32_t) * nd, hipMemcpyDeviceToHost),
+                                            "dur_len download");
+    if (rc0 == SSIM_OK && nd > 0)
+      rc0 = hip_check(hipMemcpy(dof, dataset->dur_off, sizeof(int32_t) * nd, hipMemcpyDeviceToHost), "dur_off download");
+    bool fits = rc0 == SSIM_OK;
+    for (int64_t i = 0; fits && i < nd; ++i)
+      if (dl[i] > 255 || (dl[i] > 0 && (dof[i] < 0 || dof[i] >= (1 << 24)))) fits = false;
+    h->params.hp.dcache = fits ? 1 : 0;
+    delete[] dl;
+    delete[] dof;
+    if (rc0 != SSIM_OK) {
+      delete h;
+      return rc0;
+    }
+  }
   int rc = hip_check(hipMemcpy(h->state, &h->params, sizeof(Params), hipMemcpyHostToDevice), "params upload");
   if (rc == SSIM_OK)  // both budget slots start zeroed (each budget launch then zeroes the other, TicketStop)
     rc = hip_check(hipMemset(h->state + kTicketOffset, 0, (size_t)(2 * kTicketSlotBytes)), "budget slots clear");

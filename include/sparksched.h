@@ -123,6 +123,7 @@ typedef struct ssim_layout {
   int64_t ob_acc;          /* int64    [8]             running sums over all episodes: S_act, E_act, J_act,
                                                       events popped, decisions, finished episodes, 0, 0 */
   int64_t ob_trace;       /* float64/int32 trace records, [trace_cap] x 32 B */
+  int64_t lds_bytes;       /* dynamic LDS of one engine workgroup (one env): scratch, plus the hot block if resident */
 } ssim_layout;
 
 /* indices into the per-env int32 counts block */

@@ -25,7 +25,8 @@ NSTAMPS = 6  # engine.h kTEntry, kTLoaded, kTLoopEnd, kTSaved, kTCtor, kTCopy1
 DEC_PHASES = ["(decima features)", "(decima policy)", "(decima sample copy)"]  # engine.h kPhDecFeat.. (inside policy)
 DEC_PARTS = ["[policy setup]", "[policy prep MLPs]", "[policy message passing]", "[policy DAG/global summaries]",
              "[policy stage scores]", "#nodes", "#edges", "#levels", "#schedulable", "[policy exec scores]"]
-NUM_SLOTS = 40 + NSTAMPS + len(DEC_PHASES) + len(DEC_PARTS)  # engine.h kNumPhases
+RESET_SLOTS = ["(auto-resets)", "#auto-resets"]  # engine.h kPhReset, kCtReset
+NUM_SLOTS = 40 + NSTAMPS + len(DEC_PHASES) + len(DEC_PARTS) + len(RESET_SLOTS)  # engine.h kNumPhases
 
 
 def build_prof():
@@ -97,10 +98,16 @@ def main():
                 print(f"  {name:24s} {v / dec:10.3f} per decision")
             else:
                 print(f"  {name:24s} {v / dec:10.1f} cycles/decision  {100 * v / top:5.1f}% of top-level")
+        rs = prof[:, NUM_SLOTS - 2:].cpu().numpy().astype(np.float64).sum(axis=0)
+        print(f"  {'(auto-resets)':24s} {rs[0] / dec:10.1f} cycles/decision; {int(rs[1])} resets, "
+              f"{rs[0] / max(rs[1], 1):.0f} cycles each")
         # per-wave wall clock of the launch from the realtime stamps (10 ns ticks)
         ent, loaded, loop_end, saved = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
         t0 = ent.min()
-        wall = {"entry_spread_us": float((ent.max() - t0) / 100.0),
+        ends = (saved - t0) / 100.0
+        wall = {"wave_end_us_p50": float(np.percentile(ends, 50)), "wave_end_us_p90": float(np.percentile(ends, 90)),
+                "wave_end_us_p99": float(np.percentile(ends, 99)),
+                "entry_spread_us": float((ent.max() - t0) / 100.0),
                 "load_hot_us_mean": float(((loaded - ent) / 100.0).mean()),
                 "loop_us_mean": float(((loop_end - loaded) / 100.0).mean()),
                 "save_hot_us_mean": float(((saved - loop_end) / 100.0).mean()),

@@ -44,7 +44,7 @@ def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
     out = sys.argv[2] if len(sys.argv) > 2 else None
     res = {"source": "rocprofv3 --pmc, one pass per counter group (scripts/pmc_profile.sh)", "kernels": {}}
-    for kern in ("k_rollout", "k_step"):
+    for kern in ("k_rollout", "k_step", "k_decima_rollout"):
         entry = {}
         for pas in ("waves", "icache", "fetch", "write"):
             csvp = os.path.join(root, pas, "run_counter_collection.csv")

@@ -113,6 +113,9 @@ def test_layout_structs_match_header():
             L.ob_counts, L.ob_reward, L.ob_wall_time, L.ob_acc, L.ob_trace]
     assert offs == sorted(offs) and all(o % 16 == 0 for o in offs) and L.obs_bytes >= offs[-1]
     assert len(SsimDataset._fields_) == 2 + len(DATASET_ARRAYS)
+    # the bench shape (BASELINE configs[1]) runs its 1024 single-wave workgroups one per SIMD: four envs' LDS (hot
+    # block + scratch) must fit a CU's 160 KB, or a quarter of the batch waits for a second round
+    assert L.lds_resident == 1 and 4 * L.lds_bytes <= 160 * 1024, L.lds_bytes
     cfg.num_executors = 0
     assert lib.ssim_layout_for(ctypes.byref(cfg), ctypes.byref(L)) != 0
 
