@@ -312,6 +312,8 @@ def gumbel_pick(logp: torch.Tensor, seg: torch.Tensor, nseg: int, generator=None
 
 
 class NodeEncoder(nn.Module):
+    force_dense = False  # diagnostic (scripts/profile_learner.py): the learner's encoder in the dense form too
+
     """scheduler.py:176-245 (reverse flow: children send to parents, deepest level first). Each level runs
     mlp_msg on every node and sums child messages into parents with the level's 0/1 edge weights: the same
     sums as the reference's masked sparse matmul, without data-dependent shapes."""
@@ -330,8 +332,8 @@ class NodeEncoder(nn.Module):
         parent, child = b.edge_index[0], b.edge_index[1]
         ones = torch.ones(parent.numel(), dtype=h_init.dtype, device=h_init.device)
         has_child = torch.zeros(Nt, dtype=h_init.dtype, device=h_init.device).index_add_(0, parent, ones) > 0
-        if per_obs_no_mp:  # schedule (rollouts): the dense form, whose per-row results do not depend on the batch
-            return self._dense(b, h_init, has_child, parent, child)
+        if per_obs_no_mp or self.force_dense:  # schedule (rollouts): the dense form, whose per-row results do not
+            return self._dense(b, h_init, has_child, parent, child, per_obs_no_mp)  # depend on the rest of the batch
         # evaluate_actions (the learner): the MLPs run on the rows that need them only (leaves; per level its edges'
         # children and its parents). A learner batch of J=200 observations holds millions of node rows and up to ~18
         # levels, and an MLP over every row at every level was most of the learner's time. Same values as the dense
@@ -350,7 +352,7 @@ class NodeEncoder(nn.Module):
             h = h.index_put((dst,), h_init[dst] + self.mlp_update(agg[dst]))
         return h
 
-    def _dense(self, b: DagBatch, h_init, has_child, parent, child) -> torch.Tensor:
+    def _dense(self, b: DagBatch, h_init, has_child, parent, child, per_obs_no_mp: bool = True) -> torch.Tensor:
         Nt = h_init.shape[0]
         h = torch.where(has_child[:, None], torch.zeros_like(h_init), self.mlp_update(h_init))
         for lvl in range(b.max_levels - 1, -1, -1):
@@ -359,6 +361,8 @@ class NodeEncoder(nn.Module):
             agg = torch.zeros_like(h).index_add_(0, parent, msg[child] * w[:, None])
             dst = torch.zeros(Nt, dtype=h.dtype, device=h.device).index_add_(0, parent, w) > 0
             h = torch.where(dst[:, None], h_init + self.mlp_update(agg), h)
+        if not per_obs_no_mp:
+            return h
         # schedule's convention: observations without message-passing levels keep h = mlp_prep(x)
         flat = (b.env_levels == 0)[b.node_env]
         return torch.where(flat[:, None], h_init, h)

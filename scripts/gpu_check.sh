@@ -26,10 +26,11 @@ for s in "$@"; do
     bench_nocpu) step bench_nocpu 300 python bench.py --no-cpu-baseline ;;
     bench_step) step bench_step 300 python bench.py --no-cpu-baseline --mode step ;;
     bench_decima) step bench_decima 400 python bench.py --workload decima --steps 40 --warmup 5 ;;
-    bench_ppo) step bench_ppo 900 python bench.py --workload ppo --steps 1 --warmup 0 ;;
+    bench_ppo) step bench_ppo 900 python bench.py --workload ppo --steps 2 --warmup 1 ;;
     prof_decima) step prof_decima 600 python scripts/profile_decima.py ;;
     bench_large) step bench_large 400 python bench.py --workload large --steps 100 --warmup 20 ;;
     bench_cap850) step bench_cap850 300 python bench.py --no-cpu-baseline --dataset-seed 1 ;;
+    learner) step learner 600 python scripts/profile_learner.py ;;
     prof)    step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     phase)   step phase 600 python scripts/phase_profile.py ;;
     sweep)   step sweep 900 bash scripts/steps_sweep.sh ;;

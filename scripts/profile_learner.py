@@ -1,0 +1,52 @@
+#!/usr/bin/env python
+"""Diagnostic: where one decima_tpch.yaml PPO iteration's learner time goes on the GPU (configs[4]). Collects one
+iteration's rollouts (DeviceRolloutCollector), then times PPO.train_on_rollouts with the encoder's compact and dense
+forms and prints the top device kernels / host ops of one learner pass from torch.profiler."""
+
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "gym-sparksched_amd"))
+
+
+def main():
+    import torch
+
+    from spark_sched_sim.data_samplers.synthetic_tpch import generate
+    from spark_sched_sim.schedulers import decima as D
+    from spark_sched_sim.trainers import DECIMA_TPCH, PPO
+
+    cfg = {k: dict(v) for k, v in DECIMA_TPCH.items()}
+    dev = torch.device("cuda:0")
+    ppo = PPO(cfg["agent"], cfg["env"], cfg["trainer"], dataset=generate(0), device=dev)
+    buf = ppo.collect()
+    torch.cuda.synchronize()
+    print("decisions", len(buf), flush=True)
+    state = {k: v.clone() for k, v in ppo.scheduler.state_dict().items()}
+    opt_state = ppo.scheduler.optim.state_dict()
+    for mode in ("compact", "dense", "compact"):
+        ppo.scheduler.load_state_dict(state)
+        ppo.scheduler.optim.load_state_dict(opt_state)
+        D.NodeEncoder.force_dense = mode == "dense"
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        info = ppo.train_on_rollouts(buf)
+        torch.cuda.synchronize()
+        print(f"learner ({mode} encoder): {time.perf_counter() - t0:.3f} s, {info}", flush=True)
+    D.NodeEncoder.force_dense = False
+    from torch.profiler import ProfilerActivity, profile
+
+    ppo.scheduler.load_state_dict(state)
+    ppo.scheduler.optim.load_state_dict(opt_state)
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        ppo.train_on_rollouts(buf)
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=25))
+    print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=15))
+
+
+if __name__ == "__main__":
+    main()

@@ -486,3 +486,59 @@ def test_device_collector_matches_lockstep_gpu(gpu_device, dataset):
     for k in ("stage_idx", "job_idx", "exec_idx"):
         assert torch.equal(a1[k].long(), a2[k].long()), k
     assert torch.allclose(a1["lgprob"], a2["lgprob"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_decima_rollout_preempted_collection_equals_one_launch(gpu_device, dataset):
+    """ssim_decima_rollout with a sample arena under small shared budgets with PREEMPT (steps stopped at event
+    boundaries, completed by the next launch, their rewards written into the arena then) leaves the same arena as one
+    collection launch: every record, node, edge and DAG row bit for bit (the sampling counter is the env's own
+    decision index, so launch boundaries change nothing)."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.engine import DeviceEngine
+    from spark_sched_sim.schedulers.decima import DecimaScheduler
+    from spark_sched_sim.trainers import DECIMA_TPCH
+    from spark_sched_sim.trainers.rollouts import DecimaSampleArena
+
+    env = {k: v for k, v in DECIMA_TPCH["env"].items() if k not in ("mean_time_limit", "dataset")}
+    B = 8
+    seeds = [201 + i for i in range(B)]
+    limits = np.array([np.random.RandomState(s).exponential(1.5e6) for s in seeds])
+    torch.manual_seed(5)
+    pol = DecimaScheduler(env["num_executors"]).to(gpu_device)
+    params = pol.packed_params(gpu_device)
+    arenas = []
+    for budget in (0, 3 * B):
+        eng = DeviceEngine(env, B, dataset, device=gpu_device)
+        eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=seeds, time_limits=limits)
+        arena = DecimaSampleArena(B, eng.device, cap_samples=512, cap_nodes=1 << 13, cap_edges=1 << 13,
+                                  cap_dags=1 << 11)  # small: the regions grow during the collection
+        launches, prev, grown = 0, -1, 0
+        while True:
+            if budget == 0:
+                eng.decima_rollout(params, 9, 77, 10**6, samples=arena)
+            else:
+                eng.decima_rollout(params, 9, 77, 64, budget, flags=_abi.SSIM_ROLLOUT_PREEMPT, samples=arena)
+            launches += 1
+            cur = arena.cursor.cpu().numpy()
+            if (cur[:, _abi.CUR_FULL] != 0).any():
+                arena.grow(cur)
+                grown += 1
+                continue
+            n = int(cur[:, 0].sum())
+            pend = int(np.count_nonzero(eng.views["counts"][:, _abi.OC_ERR].cpu().numpy() & _abi.SSIM_ERR_PENDING))
+            if budget == 0 or (n == prev and pend == 0):
+                break
+            prev = n
+        assert grown > 0 and (budget == 0 or launches > 10)
+        torch.cuda.synchronize()
+        arenas.append(arena)
+    a, b = arenas
+    assert torch.equal(a.cursor, b.cursor)
+    assert int(a.cursor[:, 0].min().item()) > 20
+    for i in range(B):
+        ns, nn, ne, nd = (int(x) for x in a.cursor[i, :4].tolist())
+        assert torch.equal(a.rec[i, :ns], b.rec[i, :ns]), f"env {i} records"
+        assert torch.equal(a.nodes[i, :nn], b.nodes[i, :nn]), f"env {i} nodes"
+        assert torch.equal(a.edges[i, :ne], b.edges[i, :ne]), f"env {i} edges"
+        assert torch.equal(a.dags[i, :nd], b.dags[i, :nd]), f"env {i} dags"
