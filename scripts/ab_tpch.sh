@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
 for rep in $(seq 1 "${AB_REPS:-2}"); do
-  for lib in gym-sparksched_amd/build/ab/*.so; do
+  for lib in gym-sparksched_amd/build/${AB_OUT:-ab}/*.so; do
     n=$(basename "$lib" .so)
     SSIM_LIB="$PWD/$lib" timeout -k 10 200 python bench.py --no-cpu-baseline ${AB_ARGS:-} > "gpurun_out/ab/${n}_tpch_${AB_TAG:-d}_$rep.log" 2>&1
     rc=$?

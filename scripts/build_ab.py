@@ -22,7 +22,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import __graft_entry__ as G  # noqa: E402
 
-AB = os.path.join(G.BUILD, "ab")
+AB = os.path.join(G.BUILD, os.environ.get("AB_OUT", "ab"))  # AB_OUT: another variant directory
 # translation units recompiled per variant (AB_TUS, comma-separated; default: the ABI + the bench-shape kernels)
 VARIANT_TUS = tuple(os.environ.get("AB_TUS", "sparksched.hip,k_bench900.hip").split(","))
 
