@@ -238,6 +238,8 @@ struct Sim {
   uint8_t* scr;   // this env's scratch block (LDS)
   uint8_t* obs;   // obs arena base
   int32_t eid;    // env index
+  bool res;       // hot block LDS-resident
+  bool row_lds;   // observe()'s stage -> row map in the LDS scratch (else in the cold block; StateOffsets::row_of_lds)
   EnvHeader h;    // register copy of the header
   Pcg64 rng;
   uint32_t iv_lane;  // Params::iv row `lane` (device: read with v_readlane instead of a scalar-cache load)
@@ -294,7 +296,8 @@ struct Sim {
         ghot(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         cold(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes + O.hot_bytes),
-        scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index) {
+        scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index), res(resident),
+        row_lds(resident || W::uni(p->O.row_of_lds) != 0) {
     iv_lane = W::lane() < kIvRows ? *reinterpret_cast<const uint32_t*>(IV[W::lane()]) : 0u;
     dcache_on = kDurCache && W::uni(p->hp.dcache) != 0;
     HPp = &p->hp;
@@ -1823,7 +1826,7 @@ struct Sim {
     const int src_job = source_job();
     const int16_t* act = H<int16_t>(O.active_stages);
     int16_t* sched = H<int16_t>(O.sched_list);
-    int16_t* row_of = S<int16_t>(O.sc_row_of);
+    int16_t* row_of = row_lds ? S<int16_t>(O.sc_row_of) : reinterpret_cast<int16_t*>(cold + O.row_of);
     float* nodes = reinterpret_cast<float*>(obs + HP(ob_nodes)) + (int64_t)eid * SC * 3;
     uint8_t* front = obs + HP(ob_frontier) + (int64_t)eid * SC;
     int32_t* srank = reinterpret_cast<int32_t*>(obs + HP(ob_sched_rank)) + (int64_t)eid * SC;

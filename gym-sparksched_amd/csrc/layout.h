@@ -113,7 +113,9 @@ constexpr int kNumAcc = 8;     // int64 accumulators per env in the obs arena (o
 constexpr int kTraceBytes = 32;
 constexpr int64_t kResetHeadBytes = 64;  // ssim_reset_record padded
 static_assert(sizeof(ssim_reset_record) <= kResetHeadBytes, "reset record");
-constexpr int64_t kLdsBudget = 64 * 1024;  // dynamic LDS per workgroup without opt-in
+constexpr int64_t kLdsBudget = 64 * 1024;
+constexpr int64_t kLdsPerCu = 160 * 1024;     // gfx950 LDS per CU
+constexpr int64_t kHbmWorkgroupsPerCu = 16;   // HBM-resident engine kernels: 4 one-wave workgroups per SIMD  // dynamic LDS per workgroup without opt-in
 // Opt-in dynamic LDS of one workgroup on gfx950 (a CU's 160 KB). The LDS-resident engine kernels use it for batches
 // small enough that one env per CU costs nothing (num_envs <= kBigLdsMaxEnvs, one wave per CU), e.g. the 16 envs of a
 // decima_tpch.yaml PPO iteration, whose J=200 / N=50 hot block (~146 KB) otherwise stays in HBM.
@@ -137,13 +139,14 @@ static_assert(sizeof(TraceRec) == kTraceBytes, "trace record size");
 struct StateOffsets {
   int64_t hot_bytes, cold_bytes, scratch_bytes, env_bytes;
   int64_t lds_bytes;        // scratch (+ hot when LDS-resident); decided by compute_layout
-  int32_t lds_resident, pad;
+  int32_t lds_resident, row_of_lds;  // row_of_lds: observe()'s stage -> row map in the LDS scratch (sc_row_of)
   int64_t hdr, acc, jobs, jtimes, active_jobs, picks, execs, sel_list, commits, stages, pools, active_stages,
       sched_list;
-  int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/;
+  int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/, row_of /*cold int16[S]*/;
   int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
-      sc_row_of /*int16[S]*/, sc_dcache /*uint32[N][24] when N <= kDurCacheMaxExecs*/,
-      sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build only*/;
+      sc_dcache /*uint32[N][24] when N <= kDurCacheMaxExecs*/, sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build
+      only*/, sc_row_of /*int16[S], last: LDS-resident kernels only*/;
+  int64_t scratch_hbm_bytes;  // the scratch without sc_row_of: what an HBM-resident kernel allocates
 };
 
 constexpr int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
@@ -195,6 +198,8 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   c = align16(c + 8 * S);
   O.pool_tab = c;
   c = align16(c + T * P);
+  O.row_of = c;  // observe()'s stage -> row map of the HBM-resident kernels (their LDS holds only the small scratch)
+  c = align16(c + 2 * S);
   O.cold_bytes = c;
   O.env_bytes = O.hot_bytes + O.cold_bytes;
 
@@ -211,14 +216,15 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   s = align16(s + T);
   O.sc_tab_p = s;
   s = align16(s + T);
-  O.sc_row_of = s;
-  s = align16(s + 2 * S);
   O.sc_dcache = s;  // engine.h duration-descriptor cache (kernels specialised on few executors)
   s = align16(s + (N <= kDurCacheMaxExecs ? 4 * 24 * N : 0));
   O.sc_prof = s;
 #ifdef SSIM_PROFILE
   s += 8 * 64;
 #endif
+  O.scratch_hbm_bytes = align16(s);
+  O.sc_row_of = O.scratch_hbm_bytes;
+  s = align16(O.sc_row_of + 2 * S);
   O.scratch_bytes = s;
   return O;
 }
@@ -253,7 +259,13 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
   O->lds_resident = (!(cfg.flags & SSIM_CFG_FORCE_HBM) && (need <= kLdsBudget || (need <= kLdsBudgetBig && B <= kBigLdsMaxEnvs)))
                         ? 1 : 0;
   L->lds_resident = O->lds_resident;
-  O->lds_bytes = O->scratch_bytes + (O->lds_resident ? O->hot_bytes : 0);
+  // An HBM-resident kernel (4 waves per SIMD: 16 workgroups per CU) whose full scratch would not let 16 workgroups
+  // share the CU's LDS keeps the stage -> row map in its cold block instead: 2 B per stage less LDS per wave
+  // (configs[3]'s J=200 / N=100 shard: 11 KB -> 4 KB, occupancy 3.5 -> 4 waves per SIMD, +6.5%; the Decima rollout's
+  // 9.3 KB fits and keeps the LDS map, profiles/r03/ab_row_of_cold.log).
+  O->row_of_lds = (O->lds_resident || O->scratch_bytes * kHbmWorkgroupsPerCu <= kLdsPerCu) ? 1 : 0;
+  O->lds_bytes = O->lds_resident ? O->hot_bytes + O->scratch_bytes
+                                 : O->row_of_lds ? O->scratch_bytes : O->scratch_hbm_bytes;
   L->lds_bytes = O->lds_bytes;
 
   // obs arena: each field is [B][per-env]
