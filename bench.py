@@ -229,11 +229,13 @@ def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0,
 
 # ------------------------------------------------------------------------------------------------ PMC lookup
 def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisions_per_launch: float,
-                dataset_seed: int = 0):
+                dataset_seed: int = 0, build_id: str | None = None):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*/pmc_summary*.json,
     made by scripts/pmc_profile.sh + scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
-    separate passes), scaled from bytes/decision to this launch; plus the summary's issue counters per decision
-    when present. (None, None, None) if no summary matches the config."""
+    separate passes) of the SAME BUILD (the library's ssim_build_id, recorded in the summary from the bench line
+    of its passes) and config, scaled from bytes/decision to this launch; plus the summary's issue counters per
+    decision when present. (None, None, None) if no summary of this build matches the config: a summary of another
+    build is never quoted for this one."""
     import glob
 
     best = None
@@ -245,7 +247,8 @@ def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisi
         cfg = k.get("config") or {}
         spl = cfg.get("steps_per_launch", k.get("steps") if mode == "rollout" else 1)
         if (cfg.get("mode") == mode and cfg.get("envs_per_gpu") == envs and spl == steps_per_launch
-                and cfg.get("dataset_seed", 0) == dataset_seed and "hbm_bytes_per_decision" in k):
+                and cfg.get("dataset_seed", 0) == dataset_seed and "hbm_bytes_per_decision" in k
+                and k.get("build_id") == build_id):
             best = (path, k)
     if best is None:
         return None, None, None
@@ -292,6 +295,11 @@ def run_ppo(args, rank, world, local, dev):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    from spark_sched_sim.distributed import gather_env_stats
+
+    per_rank = gather_env_stats(torch.tensor([[float(rank), elapsed, float(dec)]], dtype=torch.float64, device=dev),
+                                world).cpu().tolist()
+    ranks_seen = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     stats = reduce_timing(torch.tensor([elapsed, float(dec)], dtype=torch.float64, device=dev), world)
     elapsed, dec = stats.tolist()
     line = None
@@ -306,7 +314,8 @@ def run_ppo(args, rank, world, local, dev):
             "config": {"workload": WORKLOADS["ppo"]["desc"].format(B=B), "rows_global": B,
                        "mean_time_limit": cfg["env"]["mean_time_limit"], "mode": "ppo",
                        "parallelism": f"rows split over {world} ranks, one learner"},
-            "decisions": int(dec), "seconds_per_iteration": elapsed / args.steps,
+            "decisions": int(dec), "seconds_per_iteration": elapsed / args.steps, "ranks_seen": ranks_seen,
+            "per_rank": [{"rank": int(r), "elapsed_s": e, "decisions": int(d)} for r, e, d in per_rank],
             "phase_seconds_rank0": phases, "last_learning_stats": learn,
             "roofline": None, "cpu_baseline": None}
         if not args.no_cpu_baseline and world == 1:
@@ -370,6 +379,11 @@ def main():
     from spark_sched_sim.distributed import gather_env_stats, rank_world, reduce_timing, shard_seeds
 
     host = args.engine == "host"
+    build_id = None
+    if not host:
+        from spark_sched_sim import native
+
+        build_id = native.build_id()
     rank, world, local = rank_world()
     if world > 1:
         if host:
@@ -529,6 +543,11 @@ def main():
     elapsed = t1 - t0
     stats = torch.tensor([elapsed, decisions, alg_bytes, kern_ms, float(errs), episodes_done, float(d_acc[3])],
                          dtype=torch.float64, device=dev)
+    # what each rank measured (gathered off the timed path), so a multi-GPU line shows how many ranks the process
+    # group held and that the per-rank decisions add up to the total
+    per_rank = gather_env_stats(torch.tensor([[float(rank), elapsed, decisions, kern_ms]], dtype=torch.float64,
+                                             device=dev), world).cpu().tolist()
+    ranks_seen = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     stats = reduce_timing(stats, world)
     mine = torch.tensor(counts1[:, [_abi.OC_NUM_COMPLETED, _abi.OC_NUM_ARRIVED, _abi.OC_DECISIONS]],
                         dtype=torch.int32, device=dev)
@@ -544,11 +563,15 @@ def main():
             kern_ms = kern_ms_sum / world
             achieved = (alg_bytes / world / launches) / (kern_ms / launches / 1e3) / 1e9  # GB/s per GPU
             traffic, traffic_src, pmc = pmc_traffic(kernel, mode, B, K if (mode == "rollout" or persistent) else 1,
-                                                   decisions / world / launches, args.dataset_seed)
+                                                   decisions / world / launches, args.dataset_seed, build_id)
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                         "kernel": kernel, "kernel_ms_per_launch": kern_ms / launches,
                         "alg_bytes_per_launch": alg_bytes / world / launches}
+            if traffic is None:
+                roofline["traffic_note"] = f"no committed PMC summary of build {build_id} for this config"
+            else:
+                roofline["traffic_over_algorithmic"] = traffic / (alg_bytes / world / launches)
             if pmc is not None and "issue" in pmc:
                 # the bound that binds: instruction issue of one wave per SIMD
                 iss = dict(pmc["issue"])
@@ -568,6 +591,7 @@ def main():
             "dtype": "f64+i32",
             "data": "synthetic TPC-H-format dataset (seeded generator), " + (
                 "Decima GNN policy, random-init weights" if mode == "decima" else "random valid actions (device RNG)"),
+            "build_id": build_id,
             "config": {"workload": wl["desc"].format(B=B), "envs_per_gpu": B,
                        "jobs": cfg["job_arrival_cap"], "executors": cfg["num_executors"],
                        "mean_time_limit": wl["mean_time_limit"], "mode": mode,
@@ -594,6 +618,9 @@ def main():
             "frozen_envs": int(errs),
             "jobs_completed": int(gathered[:, 0].sum().item()),
             "jobs_arrived": int(gathered[:, 1].sum().item()),
+            "ranks_seen": ranks_seen,
+            "per_rank": [{"rank": int(r), "elapsed_s": e, "decisions": int(d), "kernel_ms": k}
+                         for r, e, d, k in per_rank],
             "roofline": roofline,
             "cpu_baseline": None,
         }

@@ -57,14 +57,35 @@ struct DecimaPolicy {
   const uint8_t* obs;
   DecimaRolloutArgs a;
 
+  // Whether act() goes on to choose an action (rollout_body asks before it claims a budgeted decision): not when the
+  // collector's episode is over (terminated, truncated by its StochasticTimeLimit, or frozen) or when the sample arena
+  // cannot hold the current observation (the region-full mark is set for the host, which grows the arena and launches
+  // again).
+  template <class S>
+  __device__ __forceinline__ bool can_act(const S& s) const {
+    using W = WaveHip;
+    if (!a.autoreset && (s.h.terminated || s.frozen() || s.h.wall >= s.h.time_limit || s.h.num_jobs == 0))
+      return false;
+    const ssim_decima_samples& sm = a.smp;
+    if (sm.rec == nullptr) return true;
+    const int32_t* cnt = reinterpret_cast<const int32_t*>(obs + P->L.ob_counts) + (int64_t)s.eid * SSIM_NUM_COUNTS;
+    int32_t* cur = sm.cursor + (int64_t)s.eid * 8;
+    if (W::uni(cur[0]) + 1 > sm.cap_samples || W::uni(cur[1]) + W::uni(cnt[SSIM_OC_NUM_NODES]) > sm.cap_nodes ||
+        W::uni(cur[2]) + W::uni(cnt[SSIM_OC_NUM_EDGES]) > sm.cap_edges ||
+        W::uni(cur[3]) + W::uni(cnt[SSIM_OC_NUM_JOBS]) > sm.cap_dags) {
+      W::sync();
+      if (W::lane() == 0) cur[4] = 1;  // region full: the host grows the arena and launches again
+      W::sync();
+      return false;
+    }
+    return true;
+  }
   template <class S>
   __device__ __forceinline__ bool act(S& s, int /*k*/, StepIn* out) const {
     using W = WaveHip;
     const ssim_layout& L = P->L;
     const int eid = s.eid;
-    // the collector's episode is over (terminated, truncated by its StochasticTimeLimit, or frozen): no more decisions
-    if (!a.autoreset && (s.h.terminated || s.frozen() || s.h.wall >= s.h.time_limit || s.h.num_jobs == 0))
-      return false;
+    // (rollout_body calls can_act() first: an arena-full or finished env never gets here)
     const ssim_decima_samples& sm = a.smp;
     const int32_t* cnt = reinterpret_cast<const int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
     const int n = W::uni(cnt[SSIM_OC_NUM_NODES]), ne = W::uni(cnt[SSIM_OC_NUM_EDGES]);
@@ -76,12 +97,6 @@ struct DecimaPolicy {
       cn = W::uni(cur[1]);
       ce = W::uni(cur[2]);
       cg = W::uni(cur[3]);
-      if (cs + 1 > sm.cap_samples || cn + n > sm.cap_nodes || ce + ne > sm.cap_edges || cg + nj > sm.cap_dags) {
-        W::sync();
-        if (W::lane() == 0) cur[4] = 1;  // region full: the host grows the arena and launches again
-        W::sync();
-        return false;
-      }
     }
 #ifdef SSIM_PROFILE
     uint64_t tp = W::clock();

@@ -88,6 +88,10 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
 #else
 #define SSIM_COUNT(ph) (void)0
 #endif
+// Diagnostic host build only (scripts/pool_stats.py): a hook per CPython-set operation (op, table size, keys).
+#ifndef SSIM_POOL_STAT
+#define SSIM_POOL_STAT(op, size, used) (void)0
+#endif
 enum : int32_t { kPoolNone = -1, kPoolCommon = 0 };
 // trace-only kinds: a job completion (:682-697) and an executor released to the common pool (:779-782, the
 // reference's Executor.add_history(wall, -1)); with the kEvReady records they give the render history.
@@ -382,6 +386,44 @@ struct Sim {
     return {O.pools + 16 * (int64_t)(1 + JC + lo), hi - lo};
   }
   __device__ __forceinline__ Span list_span(int64_t off, int n) const { return {off, (2 * (int64_t)n + 15) >> 4}; }
+  // Lowest stage still referenced (jobs' stages are contiguous in arrival order), from the header (registers) and
+  // the fixed sections: the stages of the active jobs, and stage pools / stages a completed job can still be named by
+  // — an executor left in one of its stage pools (ex.loc), an executor moving to one of its stages (EXECUTOR_READY
+  // ev_stage), a commitment from or to one of its stage pools, the current source pool. Capped at live_hi().
+  __device__ __forceinline__ int scan_live_lo() {
+    const int16_t* aj = H<int16_t>(O.active_jobs);
+    constexpr int kNone = 0x7FFFFFFF;
+    int lo = is_stage_pool(h.source) ? pool_stage(h.source) : kNone;
+    for (int k0 = 0; k0 < h.n_active_jobs; k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      const int b = k < h.n_active_jobs ? (int)job(aj[k]).base : kNone;
+      lo = W::min_i(b < lo ? b : lo);
+    }
+    for (int k0 = 0; k0 < NE; k0 += W::kWidth) {
+      const int e = k0 + W::lane();
+      int b = kNone;
+      if (e < NE) {
+        const ExecRec x = exr(e);
+        if (is_stage_pool(x.loc)) b = pool_stage(x.loc);
+        if (x.ev_seq >= 0 && x.ev_stage >= 0 && x.ev_stage < b) b = x.ev_stage;
+      }
+      lo = W::min_i(b < lo ? b : lo);
+    }
+    for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
+      const int k = k0 + W::lane();
+      int b = kNone;
+      if (k < commit_cap_for(NE)) {
+        const CommitRec r = cm(k);
+        if (r.cnt > 0) {
+          if (is_stage_pool(r.src)) b = pool_stage(r.src);
+          if (is_stage_pool(r.dst) && pool_stage(r.dst) < b) b = pool_stage(r.dst);
+        }
+      }
+      lo = W::min_i(b < lo ? b : lo);
+    }
+    const int hi = live_hi();
+    return lo < hi ? lo : hi;
+  }
   __device__ __forceinline__ void load_hot() {
     SSIM_TIC(t0);
     if (hot != ghot) {
@@ -391,42 +433,8 @@ struct Sim {
       prof_set(kTCopy1, W::realtime());
 #endif
       load_header();
-      // lowest stage still referenced (jobs' stages are contiguous in arrival order): the stages of the active
-      // jobs, and stage pools / stages a completed job can still be named by — an executor left in one of its
-      // stage pools (ex.loc), an executor moving to one of its stages (EXECUTOR_READY ev_stage), a commitment
-      // from or to one of its stage pools, the current source pool
-      const int16_t* aj = H<int16_t>(O.active_jobs);
-      constexpr int kNone = 0x7FFFFFFF;
-      int lo = is_stage_pool(h.source) ? pool_stage(h.source) : kNone;
-      for (int k0 = 0; k0 < h.n_active_jobs; k0 += W::kWidth) {
-        const int k = k0 + W::lane();
-        const int b = k < h.n_active_jobs ? (int)job(aj[k]).base : kNone;
-        lo = W::min_i(b < lo ? b : lo);
-      }
-      for (int k0 = 0; k0 < NE; k0 += W::kWidth) {
-        const int e = k0 + W::lane();
-        int b = kNone;
-        if (e < NE) {
-          const ExecRec x = exr(e);
-          if (is_stage_pool(x.loc)) b = pool_stage(x.loc);
-          if (x.ev_seq >= 0 && x.ev_stage >= 0 && x.ev_stage < b) b = x.ev_stage;
-        }
-        lo = W::min_i(b < lo ? b : lo);
-      }
-      for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
-        const int k = k0 + W::lane();
-        int b = kNone;
-        if (k < commit_cap_for(NE)) {
-          const CommitRec r = cm(k);
-          if (r.cnt > 0) {
-            if (is_stage_pool(r.src)) b = pool_stage(r.src);
-            if (is_stage_pool(r.dst) && pool_stage(r.dst) < b) b = pool_stage(r.dst);
-          }
-        }
-        lo = W::min_i(b < lo ? b : lo);
-      }
+      live_lo = scan_live_lo();
       const int hi = live_hi();
-      live_lo = lo < hi ? lo : hi;
       const Span live[4] = {stage_span(live_lo, hi), pool_span(live_lo, hi), list_span(O.active_stages, h.n_active_stages),
                             list_span(O.sched_list, h.n_sched)};
       copy_spans(hot, ghot, live);
@@ -581,7 +589,7 @@ struct Sim {
     return st_job(p - 1 - JC);
   }
   __device__ __forceinline__ PySetMeta* pmeta(int p) const { return reinterpret_cast<PySetMeta*>(&pool(p)); }
-  __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + O.pool_tab + (int64_t)p * set_cap_for(NE); }
+  __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + O.pool_tab + (int64_t)p * tab_stride_for(NE); }
   __device__ __forceinline__ UF<int16_t> cfrom(int p) const { return {&pool(p).cfrom}; }
   __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)W::uni(pool(p).used); }
 
@@ -977,8 +985,307 @@ struct Sim {
     return n;
   }
 
+  // ---- paged tables (device waves; 64 < set_cap <= 512, i.e. 16..127 executors: configs[2] / [3]) ----
+  // A table of up to 512 slots is held 8 slots per lane, page-major: lane l holds slots l, 64 + l, ..., 448 + l as the
+  // bytes of one 64-bit value (byte g = slot 64g + l), which is also the layout of its cold-block home
+  // (layout.h tab_stride_for), so ONE 8-byte load per lane brings the whole table and a slot write is one byte store.
+  // A probe window (<= 10 consecutive slots) lies in one page or two adjacent ones: per probe step, ballots of the
+  // page's byte (EMPTY / DUMMY / key) give the window's bits with no dependent per-slot loads (the serial form staged
+  // the table through LDS and walked it one byte read at a time; N = 100 makes ~18 set operations per decision).
+  // Orders: a fresh table built by clean inserts (copy(), set(gen), a resize) whose keys are all below its size
+  // holds every key at its home slot (hash(int) = int), so its iteration order is ascending. The remaining cases have
+  // at most 64 slots (with N <= 127, copy / set(gen) / resize sizes above 64 exceed every key) and reuse the one-page
+  // lane-set functions above. Same semantics as pyset.h (pinned against CPython by tests/test_kats.py); this form is
+  // pinned against CPython directly by tests/test_gpu_sets.py (ssim_debug_set_trace) and by the GPU parity cases.
+  static constexpr bool kPagedSets = W::kWidth == 64;
+  __device__ __forceinline__ bool paged_sets() const {
+    return kPagedSets && set_cap_for(NE) > 64 && set_cap_for(NE) <= kPagedTabMax;
+  }
+  __device__ __forceinline__ static uint32_t page_byte(uint64_t v, uint32_t g) { return (uint32_t)(v >> (8 * g)) & 0xFFu; }
+  struct PagedView {
+    uint32_t mask, fill, used;
+    uint64_t v;  // this lane's slots (byte g = slot 64g + lane); EMPTY outside the table
+  };
+  __device__ __forceinline__ PagedView paged_view(int p) {
+    const int l = W::lane();
+    // the cold home is read speculatively, in parallel with the record (an inline 8-slot table ignores it)
+    const uint64_t cv = *reinterpret_cast<const uint64_t*>(ptab(p) + 8 * l);
+    const PoolRec r = pool(p);
+    uint32_t w[4];
+    __builtin_memcpy(w, &r, sizeof(w));
+    const uint32_t w0 = W::uni(w[0]), w1 = W::uni(w[1]);
+    PagedView pv;
+    pv.mask = w0 & 0xFFFFu;
+    pv.fill = w0 >> 16;
+    pv.used = w1 & 0xFFFFu;
+    const uint32_t size = pv.mask + 1;
+    if (size == 8) {
+      const uint64_t tab = ((uint64_t)w[3] << 32) | w[2];
+      pv.v = l < 8 ? (~0xFFull | ((tab >> (8 * l)) & 0xFFull)) : ~0ull;
+    } else if (size < 64) {
+      pv.v = l < (int)size ? (cv | ~0xFFull) : ~0ull;
+    } else {
+      const uint32_t np = size / 64;
+      pv.v = np < 8 ? (cv | (~0ull << (8 * np))) : cv;
+    }
+    return pv;
+  }
+  // bits r < wn of the slots i + r (one page, or two adjacent ones): EMPTY, DUMMY and `key`
+  __device__ __forceinline__ static void paged_win(uint64_t v, uint32_t i, uint32_t wn, uint32_t key, uint32_t* E,
+                                                   uint32_t* D, uint32_t* K) {
+    const uint32_t g = i >> 6, o = i & 63u;
+    const uint32_t b0 = page_byte(v, g);
+    uint64_t e = W::ballot(b0 == kSlotEmpty) >> o, d = W::ballot(b0 == kSlotDummy) >> o, k = W::ballot(b0 == key) >> o;
+    if (o + wn > 64u) {  // (o >= 55: the shifts below are < 64)
+      const uint32_t b1 = page_byte(v, g + 1);
+      e |= W::ballot(b1 == kSlotEmpty) << (64u - o);
+      d |= W::ballot(b1 == kSlotDummy) << (64u - o);
+      k |= W::ballot(b1 == key) << (64u - o);
+    }
+    const uint64_t wm = (1ull << wn) - 1ull;
+    *E = (uint32_t)(e & wm);
+    *D = (uint32_t)(d & wm);
+    *K = (uint32_t)(k & wm);
+  }
+  // CPython probe walk for `key` (lt_probe on a paged table): the slot holding key or -1; *empty = the EMPTY slot that
+  // ended the walk, *dummy = the last DUMMY seen before it (set_add_entry's freeslot; dummies = false: set_lookkey).
+  __device__ __forceinline__ static int paged_probe(uint64_t v, uint32_t mask, uint32_t key, bool dummies, int* empty,
+                                                    int* dummy) {
+    uint32_t i = key & mask, perturb = key;
+    int fd = -1;
+    for (;;) {
+      const uint32_t wn = (i + 9u <= mask) ? 10u : 1u;
+      uint32_t E, D, K;
+      paged_win(v, i, wn, key, &E, &D, &K);
+      if (!dummies) D = 0;
+      const uint32_t stop = E | K;
+      if (stop) {
+        const int f = __builtin_ctz(stop);
+        const uint32_t d = D & ((1u << f) - 1u);
+        if (d) fd = (int)i + 31 - __builtin_clz(d);
+        *dummy = fd;
+        if ((K >> f) & 1u) {
+          *empty = -1;
+          return (int)i + f;
+        }
+        *empty = (int)i + f;
+        return -1;
+      }
+      if (D) fd = (int)i + 31 - __builtin_clz(D);
+      perturb >>= 5;
+      i = (i * 5u + 1u + perturb) & mask;
+    }
+  }
+  __device__ __forceinline__ static uint64_t paged_set(uint64_t v, int slot, int val) {  // the register copy
+    const uint32_t sh = 8u * (uint32_t)(slot >> 6);
+    return W::lane() == (slot & 63) ? ((v & ~(0xFFull << sh)) | ((uint64_t)(uint8_t)val << sh)) : v;
+  }
+  __device__ __forceinline__ void paged_store(int p, uint32_t mask, int slot, int val) {  // one slot at its home
+    W::sync();
+    if (W::lane() == 0) {
+      if (mask == 7)
+        pool(p).tab[slot] = (uint8_t)val;
+      else
+        ptab(p)[8 * (slot & 63) + (slot >> 6)] = (uint8_t)val;
+    }
+    W::sync();
+  }
+  __device__ __forceinline__ void paged_write(int p, uint32_t size, uint64_t v) {  // a whole (new) table
+    const int l = W::lane();
+    W::sync();
+    if (size == 8) {
+      if (l < 8) pool(p).tab[l] = (uint8_t)v;
+    } else if (size < 64) {
+      if (l < (int)size) ptab(p)[8 * l] = (uint8_t)v;
+    } else {
+      *reinterpret_cast<uint64_t*>(ptab(p) + 8 * l) = v;
+    }
+    W::sync();
+  }
+  // the keys of a paged table as a bitmap over executor ids (k0: ids 0..63, k1: 64..127), via LDS atomics
+  __device__ __forceinline__ void paged_keys(uint64_t v, uint32_t np, uint64_t* k0, uint64_t* k1) {
+    uint32_t* bm = S<uint32_t>(O.sc_bits);
+    W::sync();
+    if (W::lane() < 4) bm[W::lane()] = 0u;
+    W::sync();
+    for (uint32_t g = 0; g < np; ++g) {
+      const uint32_t b = page_byte(v, g);
+      if (b < kSlotDummy) W::aor(bm + (b >> 5), 1u << (b & 31u));
+    }
+    W::sync();
+    const u32x4 q = *reinterpret_cast<const u32x4*>(bm);
+    *k0 = ((uint64_t)W::uni((uint32_t)q[1]) << 32) | W::uni((uint32_t)q[0]);
+    *k1 = ((uint64_t)W::uni((uint32_t)q[3]) << 32) | W::uni((uint32_t)q[2]);
+  }
+  __device__ __forceinline__ static int bits_max(uint64_t k0, uint64_t k1) {  // highest set bit, -1 if none
+    return k1 ? 127 - __builtin_clzll(k1) : k0 ? 63 - __builtin_clzll(k0) : -1;
+  }
+  // the ids of a bitmap in ascending order into out[] (lane-parallel); returns the count
+  __device__ __forceinline__ static int out_ascending(uint64_t k0, uint64_t k1, int32_t* out) {
+    const int l = W::lane(), n0 = W::popc(k0);
+    W::sync();
+    if ((k0 >> l) & 1ull) out[W::rank(k0)] = l;
+    if ((k1 >> l) & 1ull) out[n0 + W::rank(k1)] = 64 + l;
+    W::sync();
+    return n0 + W::popc(k1);
+  }
+  // the keys of a paged table in iteration (slot) order into out[], those with keep(key) only; returns the count
+  template <class Keep>
+  __device__ __forceinline__ static int paged_order(uint64_t v, uint32_t np, int32_t* out, const Keep& keep) {
+    int n = 0;
+    W::sync();
+    for (uint32_t g = 0; g < np; ++g) {
+      const uint32_t b = page_byte(v, g);
+      const bool in = b < kSlotDummy && keep(b);
+      const uint64_t m = W::ballot(in);
+      if (in) out[n + W::rank(m)] = (int32_t)b;
+      n += W::popc(m);
+    }
+    W::sync();
+    return n;
+  }
+  __device__ __forceinline__ static uint32_t pages_of(uint32_t size) { return size > 64 ? size / 64 : 1; }
+  // size of a fresh set after n sequential adds (pyset.h ps_add's resizes to > 4 * used: 8, 32, 128, 512)
+  __device__ __forceinline__ static uint32_t build_size(uint32_t n) {
+    return n <= 4 ? 8u : n <= 18 ? 32u : n <= 76 ? 128u : 512u;
+  }
+  __device__ __forceinline__ static uint32_t copy_size(uint32_t n) {  // set.copy()'s table (ps_copy_order)
+    uint32_t size = 8;
+    if (n * 5 >= 21)
+      while (size <= n * 2) size <<= 1;
+    return size;
+  }
+  // set_table_resize(minused) of pool p whose slots are `v` (n keys): clean re-insert in table order, to the new home
+  __device__ __forceinline__ void paged_resize(int p, uint64_t v, uint32_t mask, uint32_t n, uint32_t minused) {
+    uint32_t size = 8;
+    while (size <= minused) size <<= 1;
+    const uint32_t np = pages_of(mask + 1);
+    uint64_t k0, k1;
+    paged_keys(v, np, &k0, &k1);
+    const int l = W::lane();
+    uint64_t nv = ~0ull;
+    if (bits_max(k0, k1) < (int)size) {  // every key at its home slot (pages 0 and 1: ids < 128)
+      if (l < (int)size && ((k0 >> l) & 1ull)) nv = (nv & ~0xFFull) | (uint64_t)l;
+      if (64 + l < (int)size && ((k1 >> l) & 1ull)) nv = (nv & ~0xFF00ull) | ((uint64_t)(64 + l) << 8);
+    } else {  // size <= 64 (n <= 15): the one-page clean re-insert
+      int32_t* tmp = S<int32_t>(O.sc_keys_b);
+      const int nn = paged_order(v, np, tmp, [](uint32_t) { return true; });
+      const int src = l < nn ? tmp[l] : (int)kSlotEmpty;
+      const int tv = lt_reinsert(src, nn >= 64 ? ~0ull : ((1ull << nn) - 1ull), size);
+      nv = ~0xFFull | (uint64_t)(uint8_t)tv;
+    }
+    paged_write(p, size, nv);
+    lt_meta(p, size - 1, n, n);
+  }
+  __device__ __forceinline__ void pool_add_paged(int p, int e) {
+    const PagedView pv = paged_view(p);
+    int empty, dummy;
+    if (paged_probe(pv.v, pv.mask, (uint32_t)e, true, &empty, &dummy) >= 0) return;  // already present
+    if (dummy >= 0) {
+      paged_store(p, pv.mask, dummy, e);
+      lt_meta(p, pv.mask, pv.fill, pv.used + 1);
+      return;
+    }
+    if ((pv.fill + 1) * 5u >= pv.mask * 3u) {
+      paged_resize(p, paged_set(pv.v, empty, e), pv.mask, pv.used + 1, (pv.used + 1) * 4);
+      return;
+    }
+    paged_store(p, pv.mask, empty, e);
+    lt_meta(p, pv.mask, pv.fill + 1, pv.used + 1);
+  }
+  __device__ __forceinline__ bool pool_remove_paged(int p, int e) {
+    const PagedView pv = paged_view(p);
+    int empty, dummy;
+    const int slot = paged_probe(pv.v, pv.mask, (uint32_t)e, false, &empty, &dummy);
+    if (slot < 0) return false;
+    paged_store(p, pv.mask, slot, kSlotDummy);
+    lt_meta(p, pv.mask, pv.fill, pv.used - 1);
+    return true;
+  }
+  // idle_order (below) of a paged table: out[0..n) = executor ids, returns n
+  __device__ __forceinline__ int idle_order_paged(int p, int32_t* out) {
+    const PagedView pv = paged_view(p);
+    const uint32_t size = pv.mask + 1, np = pages_of(size);
+    uint64_t k0, k1;
+    paged_keys(pv.v, np, &k0, &k1);
+    const int l = W::lane();
+    const bool x0 = l < NE && exr(l).busy != 0, x1 = 64 + l < NE && exr(64 + l).busy != 0;
+    const uint64_t b0 = W::ballot(x0), b1 = W::ballot(x1);
+    const uint64_t f0 = k0 & ~b0, f1 = k1 & ~b1;
+    const int nf = W::popc(f0) + W::popc(f1);
+    if (nf == 0) return 0;
+    // set(gen) of the idle keys: a fresh set whose final size exceeds every key holds them in ascending order,
+    // whatever order the copy() yields them in
+    if (bits_max(f0, f1) < (int)build_size((uint32_t)nf)) return out_ascending(f0, f1, out);
+    // nf <= 18 from here (every larger set(gen) ends at 128 slots): the copy's order, filtered, then the adds
+    const auto idle = [&](uint32_t b) { return ((((b < 64u) ? b0 : b1) >> (b & 63u)) & 1ull) == 0ull; };
+    int32_t* tmp = S<int32_t>(O.sc_keys_b);
+    const uint32_t sc = copy_size(pv.used);
+    int kv;
+    if (sc == size && pv.fill == pv.used) {  // copy() is a slot copy: the source's order
+      paged_order(pv.v, np, tmp, idle);
+      kv = l < nf ? tmp[l] : (int)kSlotEmpty;
+    } else if (bits_max(k0, k1) < (int)sc) {  // copy() re-inserts at the home slots: ascending
+      out_ascending(f0, f1, tmp);
+      kv = l < nf ? tmp[l] : (int)kSlotEmpty;
+    } else {  // copy() of <= 31 keys into <= 64 slots: the one-page clean re-insert in the source's order
+      const int nn = paged_order(pv.v, np, tmp, [](uint32_t) { return true; });
+      const int src = l < nn ? tmp[l] : (int)kSlotEmpty;
+      const int tv = lt_reinsert(src, nn >= 64 ? ~0ull : ((1ull << nn) - 1ull), sc);
+      const bool keep = tv != (int)kSlotEmpty && idle((uint32_t)tv);
+      kv = W::compact(W::ballot(keep), tv);
+    }
+    kv = lt_build_order(kv, nf);
+    W::sync();
+    if (l < nf) out[l] = kv;
+    W::sync();
+    return nf;
+  }
+  // set(range(N)) built by sequential adds (reset's COMMON pool): every key at its home slot
+  __device__ __forceinline__ void paged_init_range(int p, int n) {
+    const uint32_t size = build_size((uint32_t)n);
+    const int l = W::lane();
+    uint64_t nv = ~0ull;
+    if (l < n && l < (int)size) nv = (nv & ~0xFFull) | (uint64_t)l;
+    if (64 + l < n && 64 + l < (int)size) nv = (nv & ~0xFF00ull) | ((uint64_t)(64 + l) << 8);
+    paged_write(p, size, nv);
+    lt_meta(p, size - 1, (uint32_t)n, (uint32_t)n);
+  }
+  // the keys of pool p in iteration order into out[] (diagnostic / the set known-answer test); returns the count
+  __device__ __forceinline__ int table_keys(int p, int32_t* out) {
+    if constexpr (kPagedSets) {
+      if (paged_sets()) {
+        const PagedView pv = paged_view(p);
+        return paged_order(pv.v, pages_of(pv.mask + 1), out, [](uint32_t) { return true; });
+      }
+    }
+    if constexpr (kLaneSets) {
+      if (lane_sets()) {
+        const PoolView pv = pool_view(p);
+        const uint64_t occ = W::ballot(pv.v < kSlotDummy) & slot_bits(pv.mask);
+        const int kv = W::compact(occ, pv.v);
+        W::sync();
+        if (W::lane() < W::popc(occ)) out[W::lane()] = kv;
+        W::sync();
+        return W::popc(occ);
+      }
+    }
+    const uint8_t* t = stage_table(p);
+    const int n = ps_keys<W>(pmeta(p), t, out);
+    W::sync();
+    return n;
+  }
+
   __device__ __forceinline__ void pool_add(int p, int e) {
+    SSIM_POOL_STAT(0, (int)W::uni(pool(p).mask) + 1, pool_size(p));
     SSIM_TIC(t0);
+    if constexpr (kPagedSets) {
+      if (paged_sets()) {
+        pool_add_paged(p, e);
+        SSIM_TOC(t0, kPhPool);
+        return;
+      }
+    }
     if constexpr (kLaneSets) {
       if (lane_sets()) {
         pool_add_lanes(p, e);
@@ -992,7 +1299,15 @@ struct Sim {
     SSIM_TOC(t0, kPhPool);
   }
   __device__ __forceinline__ void pool_remove(int p, int e) {
+    SSIM_POOL_STAT(1, (int)W::uni(pool(p).mask) + 1, pool_size(p));
     SSIM_TIC(t0);
+    if constexpr (kPagedSets) {
+      if (paged_sets()) {
+        check(pool_remove_paged(p, e));
+        SSIM_TOC(t0, kPhPool);
+        return;
+      }
+    }
     if constexpr (kLaneSets) {
       if (lane_sets()) {
         check(pool_remove_lanes(p, e));
@@ -1033,8 +1348,17 @@ struct Sim {
   // Table order of set(e for e in pool.copy() if not busy) — _get_idle_source_executors (:714-728).
   __device__ __forceinline__ int idle_order(int p, int32_t* out) {
     if (p < 0) return 0;
+    SSIM_POOL_STAT(2, (int)W::uni(pool(p).mask) + 1, pool_size(p));
     SSIM_COUNT(kCtIdleOrder);
     SSIM_TIC(t0);
+    if constexpr (kPagedSets) {
+      if (paged_sets()) {
+        const int n = idle_order_paged(p, out);
+        SSIM_TOC(t0, kPhPool);
+        SSIM_TOC(t0, kPhIdleOrder);
+        return n;
+      }
+    }
     if constexpr (kLaneSets) {
       if (lane_sets()) {
         const int n = idle_order_lanes(p, out);
@@ -2056,6 +2380,9 @@ struct Sim {
     if (!pending()) return true;
     return finish_step(take_pending(), stop);
   }
+  // The last step_begin refused its action (ValueError / KeyError in the reference): the state is untouched and no
+  // observation was written, only the error bits of the obs arena.
+  bool rejected = false;
   // step() with the header already in registers. Returns false when `stop` preempted the step's simulation (the
   // step stays pending until resume()).
   template <class Stop = NoStop>
@@ -2069,12 +2396,14 @@ struct Sim {
   // The fused rollout calls step_begin and finish_step from one loop, so finish_step (the event loop, the
   // observation) is inlined once whether a launch starts a step or completes a preempted one.
   __device__ __forceinline__ bool step_begin(StepIn a, double* t0) {
+    rejected = false;
     if (h.terminated || frozen() || h.num_jobs == 0) return false;
     SSIM_TIC(t_act);
     const int idx = a.stage_idx, nx = a.num_exec;
     // Discrete(n, start=-1) holds -1 .. n-2; Discrete(N, start=1) holds 1 .. N
     if (idx < -1 || idx > h.stage_idx_n - 2 || nx < 1 || nx > NE) {
       write_err_only(SSIM_ERR_SPACE);
+      rejected = true;
       return false;
     }
     if (idx == -1) {
@@ -2082,11 +2411,13 @@ struct Sim {
     } else {
       if (idx >= h.n_sched) {
         write_err_only(SSIM_ERR_KEY);
+        rejected = true;
         return false;
       }
       const int g = ld(H<int16_t>(O.sched_list) + idx);
       if (nx > committable()) {
         write_err_only(SSIM_ERR_TOO_MANY);
+        rejected = true;
         return false;
       }
       const int d = demand(g);
@@ -2286,7 +2617,9 @@ struct Sim {
     }
     W::sync();
     ev_regs_load();
-    {
+    if (paged_sets()) {
+      paged_init_range(kPoolCommon, NE);
+    } else {
       uint8_t* t = S<uint8_t>(O.sc_tab_p);
       ps_init(pmeta(kPoolCommon), t);
       for (int e = 0; e < NE; ++e) ps_add<W>(pmeta(kPoolCommon), t, (uint32_t)e, S<int32_t>(O.sc_keys_b));

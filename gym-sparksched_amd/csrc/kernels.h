@@ -63,6 +63,10 @@ struct TicketStop {
       __hip_atomic_store(word(1 + WaveHip::lane()), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
+  // Returns `n` decisions granted to this wave but not taken, so other waves of the launch can still claim them.
+  __device__ __forceinline__ void give_back(int64_t n) const {
+    if (WaveHip::lane() == 0) atomicAdd(word(0), (unsigned long long)(-n));
+  }
   __device__ __forceinline__ uint64_t issue() const {
     return on ? __hip_atomic_load(word(1 + line), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
   }
@@ -96,6 +100,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
 struct HeuristicPolicy {  // fair / FIFO / random (policy.h)
   int kind;
   uint64_t seed;
+  // whether act() would choose an action (checked before a budget claim, so a claim is never spent on an env whose
+  // policy then declines)
+  template <class S>
+  __device__ __forceinline__ bool can_act(const S&) const {
+    return true;
+  }
   template <class S>
   __device__ __forceinline__ bool act(S& s, int /*k*/, StepIn* a) const {
     *a = sim_policy(s, kind, seed);
@@ -179,13 +189,14 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
       simulate = true;
     } else {
       if (k >= num_steps) break;
+      if (!pol.can_act(s)) break;
       if (stop.base != nullptr) {
         if (!autoreset && (s.h.terminated || s.frozen())) break;
         if (granted == 0 && (granted = stop.claim(B, last)) == 0) break;
         --granted;
       }
       StepIn a;
-      if (!pol.act(s, k, &a)) break;
+      if (!pol.act(s, k, &a)) break;  // (never after can_act: a claimed decision is always taken)
 #ifdef SSIM_PROFILE
       s.prof_add(kPhPolicy, WaveHip::clock() - t0);
 #endif
@@ -196,6 +207,12 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
       ++k;
       WaveHip::sync();
       simulate = s.step_begin(a, &st0);
+      if (!simulate && s.rejected) {  // a device policy chose an invalid action: freeze the env (the host sees it)
+        s.fail(SSIM_ERR_INVARIANT);
+        s.store_header();
+        s.write_err_only(0u);
+        break;
+      }
       if (!simulate) pol.done(s);
     }
     if (simulate) {
@@ -212,6 +229,7 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
     }
 #endif
   }
+  if (granted > 0) stop.give_back(granted);  // a chunk the wave could not use (its step cap or episode end)
 #ifdef SSIM_PROFILE
   s.prof_set(kTLoopEnd, WaveHip::realtime());
 #endif

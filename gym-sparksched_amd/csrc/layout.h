@@ -113,9 +113,9 @@ constexpr int kNumAcc = 8;     // int64 accumulators per env in the obs arena (o
 constexpr int kTraceBytes = 32;
 constexpr int64_t kResetHeadBytes = 64;  // ssim_reset_record padded
 static_assert(sizeof(ssim_reset_record) <= kResetHeadBytes, "reset record");
-constexpr int64_t kLdsBudget = 64 * 1024;
+constexpr int64_t kLdsBudget = 64 * 1024;    // dynamic LDS per workgroup without opt-in
 constexpr int64_t kLdsPerCu = 160 * 1024;     // gfx950 LDS per CU
-constexpr int64_t kHbmWorkgroupsPerCu = 16;   // HBM-resident engine kernels: 4 one-wave workgroups per SIMD  // dynamic LDS per workgroup without opt-in
+constexpr int64_t kHbmWorkgroupsPerCu = 16;   // HBM-resident engine kernels: 4 one-wave workgroups per SIMD
 // Opt-in dynamic LDS of one workgroup on gfx950 (a CU's 160 KB). The LDS-resident engine kernels use it for batches
 // small enough that one env per CU costs nothing (num_envs <= kBigLdsMaxEnvs, one wave per CU), e.g. the 16 envs of a
 // decima_tpch.yaml PPO iteration, whose J=200 / N=50 hot block (~146 KB) otherwise stays in HBM.
@@ -144,7 +144,7 @@ struct StateOffsets {
       sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/, row_of /*cold int16[S]*/;
   int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
-      sc_dcache /*uint32[N][24] when N <= kDurCacheMaxExecs*/, sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build
+      sc_dcache /*uint32[N][24] when N <= kDurCacheMaxExecs*/, sc_bits /*uint32[4]*/, sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build
       only*/, sc_row_of /*int16[S], last: LDS-resident kernels only*/;
   int64_t scratch_hbm_bytes;  // the scratch without sc_row_of: what an HBM-resident kernel allocates
 };
@@ -157,13 +157,21 @@ constexpr int set_cap_for(int n) {  // smallest power of two > 4N (max CPython s
   return c;
 }
 constexpr int commit_cap_for(int n) { return 2 * n + 2; }
+// Bytes per pool in the cold block's table area. Tables of up to 512 slots (executor counts 16..127) are stored
+// page-major for the device's lane-parallel set operations (engine.h "paged tables": slot s at byte
+// 8 * (s % 64) + s / 64, so lane l reads its 8 slots with one 8-byte load), which takes the full 512 bytes whatever
+// the current capacity; smaller and larger capacities keep slot order (byte s = slot s).
+constexpr int kPagedTabMax = 512;
+constexpr int tab_stride_for(int n) {
+  return set_cap_for(n) > 64 && set_cap_for(n) <= kPagedTabMax ? kPagedTabMax : set_cap_for(n);
+}
 constexpr int64_t kDurCacheMaxExecs = 16;
 
 // The per-env block layout as a function of (N, J, S). Single source of truth for the host layout and for
 // the device engine, which re-derives it with N and J as compile-time constants where it can.
 constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   StateOffsets O{};
-  const int64_t P = 1 + J + S, T = set_cap_for((int)N), C = commit_cap_for((int)N);
+  const int64_t P = 1 + J + S, T = set_cap_for((int)N), C = commit_cap_for((int)N), TS = tab_stride_for((int)N);
   int64_t o = 0;
   O.hdr = o;
   o = align16(o + (int64_t)sizeof(EnvHeader));
@@ -197,7 +205,7 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   O.st_recent = c;
   c = align16(c + 8 * S);
   O.pool_tab = c;
-  c = align16(c + T * P);
+  c = align16(c + TS * P);
   O.row_of = c;  // observe()'s stage -> row map of the HBM-resident kernels (their LDS holds only the small scratch)
   c = align16(c + 2 * S);
   O.cold_bytes = c;
@@ -218,6 +226,8 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   s = align16(s + T);
   O.sc_dcache = s;  // engine.h duration-descriptor cache (kernels specialised on few executors)
   s = align16(s + (N <= kDurCacheMaxExecs ? 4 * 24 * N : 0));
+  O.sc_bits = s;  // uint32[4]: a set's keys as a bitmap over executor ids (paged-table operations)
+  s = align16(s + (T > 64 && T <= kPagedTabMax ? 16 : 0));
   O.sc_prof = s;
 #ifdef SSIM_PROFILE
   s += 8 * 64;

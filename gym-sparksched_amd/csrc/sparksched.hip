@@ -9,6 +9,8 @@
 //   k_rollout : `num_steps` x (policy -> step) fused into one launch (no host round trips)
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+
+#include <mutex>
 #include <stdio.h>
 #include <string.h>
 
@@ -86,6 +88,40 @@ __global__ __launch_bounds__(64) void k_decima_policy(const Params* __restrict__
     atomicAdd(overflow, 1);
 }
 
+// Test hook (tests/test_gpu_sets.py, ssim_debug_set_trace): a trace of CPython-set operations on one pool (job 0's)
+// of env 0, through the engine's own set code on the path the layout selects (one-page lane sets for <= 15
+// executors, paged tables for 16..127, the serial form beyond). ops: int32 [n_ops][6] = (code, key, busy bitmap
+// words 0..3); code 0 add(key), 1 remove(key), 2 idle order: list(set(e for e in s.copy() if not busy[e])) with the
+// executors' busy flags set from the bitmap. orders [n_ops][width]: the set's iteration order after an add / remove,
+// the idle order for code 2; -1 padded.
+__global__ __launch_bounds__(64) void k_debug_set_trace(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+                                                        const int32_t* __restrict__ ops, int n_ops, int width,
+                                                        int32_t* orders) {
+  Sim<WaveHip> s(P, state, g_smem, obs, 0, false);
+  const int p = s.job_pool(0);
+  ps_init(s.pmeta(p), s.pool(p).tab);
+  int32_t* out = s.template S<int32_t>(s.O.sc_keys_a);
+  for (int k = 0; k < n_ops; ++k) {
+    const int code = WaveHip::uni(ops[6 * k]), key = WaveHip::uni(ops[6 * k + 1]);
+    int n = 0;
+    if (code == 2) {
+      for (int e = WaveHip::lane(); e < s.NE; e += 64)
+        s.exr(e).busy = (int16_t)((ops[6 * k + 2 + (e >> 5)] >> (e & 31)) & 1);
+      WaveHip::sync();
+      n = s.idle_order(p, out);
+    } else {
+      if (code == 0)
+        s.pool_add(p, key);
+      else
+        s.pool_remove(p, key);
+      n = s.table_keys(p, out);
+    }
+    WaveHip::sync();
+    for (int i = WaveHip::lane(); i < width; i += 64) orders[(int64_t)k * width + i] = i < n ? out[i] : -1;
+    WaveHip::sync();
+  }
+}
+
 // per-job arrival/completion times and state (JobRec/JobTimes in the hot block) -> [num_envs][job_cap]
 __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, const uint8_t* state,
                                                   double* ta, double* tc, int32_t* st) {
@@ -146,7 +182,9 @@ static int hip_check(hipError_t e, const char* what) {
 
 // A launch with more than 64 KB of dynamic LDS (layout.h kLdsBudgetBig) needs the kernel's opt-in attribute. It is
 // per-device, per-function state: the raised limit is remembered per (device, kernel) so the attribute call is made
-// once, not before every step launch (a small cache; a miss or a race at worst repeats the idempotent call).
+// once, not before every step launch. The cache is shared by every host thread that launches, so it is guarded by a
+// mutex (an unguarded entry could pair one kernel with another thread's larger limit and skip a needed call).
+static std::mutex g_lds_mu;
 static int lds_opt_in(const void* fn, int64_t lds) {
   if (lds <= kLdsBudget) return SSIM_OK;
   struct Entry {
@@ -159,7 +197,8 @@ static int lds_opt_in(const void* fn, int64_t lds) {
   int dev = 0;
   int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
   if (rc != SSIM_OK) return rc;
-  for (int i = 0; i < n_cache && i < 64; ++i)
+  std::lock_guard<std::mutex> lk(g_lds_mu);
+  for (int i = 0; i < n_cache; ++i)
     if (cache[i].dev == dev && cache[i].fn == fn && cache[i].lds >= lds) return SSIM_OK;
   rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                  "engine kernel LDS attribute");
@@ -363,7 +402,7 @@ extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed
 // Diagnostic build only: the budget rollout (as bench.py) with per-wave phase sums and realtime stamps.
 extern "C" int ssim_rollout_budget_profiled(ssim_handle* h, int32_t kind, uint64_t seed, int32_t max_steps,
                                             int64_t total_decisions, int32_t flags, uint64_t* prof_out,
-                                            void* stream) {
+                                            const double* time_limits, void* stream) {
   const ssim_layout& L = h->params.L;
   if (total_decisions <= 0) return set_err(SSIM_E_ARG, "ssim_rollout_budget_profiled: total_decisions must be > 0");
   const RolloutFn fn = pick_rollout(h->params);
@@ -371,7 +410,7 @@ extern "C" int ssim_rollout_budget_profiled(ssim_handle* h, int32_t kind, uint64
   if (rc != SSIM_OK) return rc;
   if (h->ticket_slot) flags |= kFlagTicketSlot;
   hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
-                     dparams(h), h->state, h->obs, kind, seed, max_steps, flags, (const double*)nullptr, h->reset,
+                     dparams(h), h->state, h->obs, kind, seed, max_steps, flags, time_limits, h->reset,
                      (int32_t*)nullptr, prof_out, total_decisions, (const int32_t*)nullptr);
   const int rc2 = hip_check(hipGetLastError(), "k_rollout(budget, profiled) launch");
   if (rc2 == SSIM_OK) h->ticket_slot ^= 1;
@@ -392,6 +431,17 @@ extern "C" int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_compl
   hipLaunchKernelGGL(k_job_times, dim3(h->params.L.num_envs), dim3(64), 0, (hipStream_t)stream, dparams(h), h->state,
                      t_arrival, t_completed, state);
   return hip_check(hipGetLastError(), "k_job_times launch");
+}
+
+extern "C" int ssim_debug_set_trace(ssim_handle* h, const int32_t* ops, int32_t n_ops, int32_t width, int32_t* orders,
+                                    void* stream) {
+  if (h == nullptr || ops == nullptr || orders == nullptr || n_ops < 0 || width <= 0)
+    return set_err(SSIM_E_ARG, "ssim_debug_set_trace: bad argument");
+  if (h->params.L.num_executors > 127 || h->params.L.job_cap < 1)
+    return set_err(SSIM_E_ARG, "ssim_debug_set_trace: needs 1..127 executors and a job cap >= 1");
+  hipLaunchKernelGGL(k_debug_set_trace, dim3(1), dim3(64), (size_t)h->params.L.scratch_bytes, (hipStream_t)stream,
+                     dparams(h), h->state, h->obs, ops, n_ops, width, orders);
+  return hip_check(hipGetLastError(), "k_debug_set_trace launch");
 }
 
 extern "C" int ssim_decima_features(ssim_handle* h, float num_tasks_scale, float work_scale, float* node_feats,
@@ -448,20 +498,9 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
                        h->policy_plan, stride);
     return hip_check(hipGetLastError(), "k_decima_policy(global plan) launch");
   }
-  if (lds > 64 * 1024) {
-    // hipFuncSetAttribute is per-device state: remember the raised limit per device (a process may drive
-    // several GPUs); the cache is a fast path only, a race at worst repeats the (idempotent) call
-    static int64_t configured[64] = {0};
-    int dev = 0;
-    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+  {
+    const int rc = lds_opt_in((const void*)k_decima_policy<false>, lds);
     if (rc != SSIM_OK) return rc;
-    if (dev < 0 || dev >= 64 || lds > configured[dev]) {
-      rc = hip_check(hipFuncSetAttribute((const void*)k_decima_policy<false>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                     "k_decima_policy LDS attribute");
-      if (rc != SSIM_OK) return rc;
-      if (dev >= 0 && dev < 64) configured[dev] = lds;
-    }
   }
   hipLaunchKernelGGL(k_decima_policy<false>, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream,
                      dparams(h), h->obs, node_feats, commit_cap, edge_mask, depth, params, node_cap, seed, counter,
@@ -530,3 +569,8 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
 }
 
 extern "C" const char* ssim_last_error(void) { return g_err; }
+
+#ifndef SSIM_BUILD_ID
+#define SSIM_BUILD_ID "unversioned"
+#endif
+extern "C" const char* ssim_build_id(void) { return SSIM_BUILD_ID; }

@@ -48,6 +48,9 @@ def lib() -> ct.CDLL:
     L.ssim_decima_rollout.argtypes = [vp, vp, i32, ct.c_float, ct.c_float, u64, u64, i32, ct.c_int64, i32, vp, vp,
                                       ct.c_int64, vp, vp, vp]
     L.ssim_last_error.restype = ct.c_char_p
+    L.ssim_build_id.restype = ct.c_char_p
+    L.ssim_debug_set_trace.argtypes = [vp, vp, i32, i32, vp, vp]
+    L.ssim_debug_set_trace.restype = ct.c_int
     for name in ("ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
                  "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
                  "ssim_job_times", "ssim_decima_features", "ssim_decima_policy", "ssim_decima_rollout"):
@@ -65,4 +68,9 @@ EXPORTED_SYMBOLS = ["ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_rese
                     "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
                     "ssim_job_times",
                     "ssim_decima_features", "ssim_decima_policy", "ssim_decima_workspace_bytes", "ssim_decima_rollout",
-                    "ssim_last_error"]
+                    "ssim_last_error", "ssim_build_id", "ssim_debug_set_trace"]
+
+
+def build_id() -> str:
+    """The loaded library's build identity (source + definition hash, __graft_entry__.source_hash)."""
+    return lib().ssim_build_id().decode()

@@ -167,16 +167,19 @@ def live_sizes(views: dict, feats: dict, alive: torch.Tensor):
     return ids, (int(n.sum()), int(ne.sum()), int(nj.sum()), int(levels.max()), int(n.max()))
 
 
-def select_envs(b: DagBatch, envs: torch.Tensor) -> DagBatch:
+def select_envs(b: DagBatch, envs: torch.Tensor, sizes: tuple[int, int, int, int, int] | None = None) -> DagBatch:
     """Sub-batch of the observations `envs` (i64 indices into b's env rows, any order), renumbered 0..K-1
-    in the given order (the rollout buffer keeps alive envs' observations this way)."""
+    in the given order (the rollout buffer keeps alive envs' observations this way). `sizes` (total nodes, edges,
+    DAGs, max levels, max nodes of the sub-batch; minibatch_plans) removes the host sync for them."""
     dev = b.x.device
     envs = envs.to(dev).long()
     K = envs.numel()
     n, ne = b.num_nodes[envs], b.num_edges[envs]
     nd = (b.obs_ptr[1:] - b.obs_ptr[:-1])[envs]
     lv = b.env_levels[envs]
-    if K == 0:
+    if sizes is not None:
+        Nt, Et, Gt, L, Nmax = sizes
+    elif K == 0:
         Nt = Et = Gt = L = Nmax = 0
     else:
         Nt, Et, Gt, L, Nmax = (int(v) for v in torch.stack([n.sum(), ne.sum(), nd.sum(), lv.max(),
@@ -197,6 +200,63 @@ def select_envs(b: DagBatch, envs: torch.Tensor) -> DagBatch:
                     stage_mask=b.stage_mask[src_node], exec_cap=b.exec_cap[src_dag],
                     num_stage_acts=b.num_stage_acts[envs], num_nodes=n, num_edges=ne, num_envs=K,
                     max_nodes=Nmax)
+
+
+def learner_counts(b: DagBatch) -> torch.Tensor:
+    """Per observation of b, the sizes of the compact learner path's index sets (NodeEncoder / scores_all with a
+    plan): i64 [B, 2 + 2L] = leaves, schedulable rows, then per message-passing level l < b.max_levels the level's
+    edges and its distinct parents. A sub-batch's sizes are sums over its observations, so the sizes of every
+    minibatch of an epoch come from one host sync (minibatch_plans) instead of one per index set."""
+    dev = b.x.device
+    Nt, B, L = b.x.shape[0], b.num_envs, b.max_levels
+    parent = b.edge_index[0]
+    has_child = torch.zeros(Nt, dtype=torch.long, device=dev).index_add_(
+        0, parent, torch.ones_like(parent)) > 0
+    cols = [segment_sum((~has_child).long(), b.node_env, B), segment_sum(b.stage_mask.long(), b.node_env, B)]
+    edge_env = b.node_env[parent] if parent.numel() else parent
+    for lvl in range(L):
+        on = ((b.edge_bits >> lvl) & 1).long()
+        cols.append(segment_sum(on, edge_env, B))
+        dst = torch.zeros(Nt, dtype=torch.long, device=dev).index_add_(0, parent, on) > 0
+        cols.append(segment_sum(dst.long(), b.node_env, B))
+    return torch.stack(cols, dim=1)
+
+
+@dataclass
+class LearnerPlan:
+    """Host sizes of one sub-batch's compact index sets (see learner_counts)."""
+    leaves: int
+    sched: int
+    edges: list[int]
+    dsts: list[int]
+
+
+def minibatch_plans(b: DagBatch, counts: torch.Tensor, groups: list[torch.Tensor]):
+    """For each env-index group (a minibatch of b's observations): the select_envs `sizes` and the LearnerPlan of
+    the sub-batch, all in ONE host sync. Returns [(sizes, plan)] in group order."""
+    dev = b.x.device
+    if not groups:
+        return []
+    nd = b.obs_ptr[1:] - b.obs_ptr[:-1]
+    per_env = torch.cat([torch.stack([b.num_nodes, b.num_edges, nd], dim=1), counts], dim=1)  # summed columns
+    gid = torch.cat([torch.full((g.numel(),), k, dtype=torch.long, device=dev) for k, g in enumerate(groups)])
+    rows = torch.cat([g.to(dev).long() for g in groups])
+    G = len(groups)
+    sums = torch.zeros((G, per_env.shape[1]), dtype=torch.long, device=dev).index_add_(0, gid, per_env[rows])
+    mx = torch.zeros((G, 2), dtype=torch.long, device=dev).scatter_reduce_(
+        0, gid[:, None].expand(-1, 2), torch.stack([b.env_levels[rows], b.num_nodes[rows]], dim=1), reduce="amax",
+        include_self=True)
+    host = torch.cat([sums, mx], dim=1).cpu().tolist()
+    out = []
+    L = counts.shape[1] // 2 - 1
+    for r in host:
+        Nt, Et, Gt = r[0], r[1], r[2]
+        c = r[3:3 + counts.shape[1]]
+        Lg, Nmax = r[-2], r[-1]
+        plan = LearnerPlan(leaves=c[0], sched=c[1], edges=[c[2 + 2 * l] for l in range(L)],
+                           dsts=[c[3 + 2 * l] for l in range(L)])
+        out.append(((Nt, Et, Gt, Lg, Nmax), plan))
+    return out
 
 
 def cat_batches(bs: list[DagBatch]) -> DagBatch:
@@ -312,11 +372,11 @@ def gumbel_pick(logp: torch.Tensor, seg: torch.Tensor, nseg: int, generator=None
 
 
 class NodeEncoder(nn.Module):
-    force_dense = False  # diagnostic (scripts/profile_learner.py): the learner's encoder in the dense form too
-
     """scheduler.py:176-245 (reverse flow: children send to parents, deepest level first). Each level runs
     mlp_msg on every node and sums child messages into parents with the level's 0/1 edge weights: the same
     sums as the reference's masked sparse matmul, without data-dependent shapes."""
+
+    force_dense = False  # the learner's encoder in the dense form too (tests, scripts/profile_learner.py)
 
     def __init__(self, num_node_features: int, embed_dim: int, mlp_kwargs: dict[str, Any]):
         super().__init__()
@@ -324,7 +384,7 @@ class NodeEncoder(nn.Module):
         self.mlp_msg = make_mlp(embed_dim, output_dim=embed_dim, **mlp_kwargs)
         self.mlp_update = make_mlp(embed_dim, output_dim=embed_dim, **mlp_kwargs)
 
-    def forward(self, b: DagBatch, per_obs_no_mp: bool) -> torch.Tensor:
+    def forward(self, b: DagBatch, per_obs_no_mp: bool, plan: LearnerPlan | None = None) -> torch.Tensor:
         h_init = self.mlp_prep(b.x)
         if b.max_levels == 0:
             return h_init  # _forward_no_mp for every observation
@@ -340,15 +400,30 @@ class NodeEncoder(nn.Module):
         # form up to the GEMM shapes (the reference's masked sparse matmul sums the level's child messages into their
         # parents); rollouts keep the dense form so a row's actions and log-probs do not depend on which other rows
         # share its batch (the multi-rank learner's bit-equality with one rank).
-        leaves = torch.nonzero(~has_child).squeeze(1)
+        # With a plan (the PPO learner's minibatches) the index sets' sizes are known on the host, so the sets come
+        # from nonzero_static and the forward issues no host sync.
+        if plan is not None:
+            leaves = torch.nonzero_static(~has_child, size=plan.leaves).squeeze(1)
+        else:
+            leaves = torch.nonzero(~has_child).squeeze(1)
         h = torch.zeros_like(h_init).index_put((leaves,), self.mlp_update(h_init[leaves]))
         for lvl in range(b.max_levels - 1, -1, -1):
-            eidx = torch.nonzero((b.edge_bits >> lvl) & 1).squeeze(1)
-            if eidx.numel() == 0:
-                continue
+            on = (b.edge_bits >> lvl) & 1
+            if plan is not None:
+                if plan.edges[lvl] == 0:
+                    continue
+                eidx = torch.nonzero_static(on, size=plan.edges[lvl]).squeeze(1)
+            else:
+                eidx = torch.nonzero(on).squeeze(1)
+                if eidx.numel() == 0:
+                    continue
             p, c = parent[eidx], child[eidx]
             agg = torch.zeros_like(h).index_add_(0, p, self.mlp_msg(h[c]))
-            dst = torch.unique(p)
+            if plan is not None:  # the level's distinct parents, ascending (= torch.unique)
+                hit = torch.zeros(Nt, dtype=torch.long, device=p.device).index_add_(0, p, torch.ones_like(p)) > 0
+                dst = torch.nonzero_static(hit, size=plan.dsts[lvl]).squeeze(1)
+            else:
+                dst = torch.unique(p)
             h = h.index_put((dst,), h_init[dst] + self.mlp_update(agg[dst]))
         return h
 
@@ -399,8 +474,8 @@ class EncoderNetwork(nn.Module):
         self.dag_encoder = DagEncoder(num_node_features, embed_dim, mlp_kwargs)
         self.global_encoder = GlobalEncoder(embed_dim, mlp_kwargs)
 
-    def forward(self, b: DagBatch, per_obs_no_mp: bool) -> dict[str, torch.Tensor]:
-        h_node = self.node_encoder(b, per_obs_no_mp)
+    def forward(self, b: DagBatch, per_obs_no_mp: bool, plan: LearnerPlan | None = None) -> dict[str, torch.Tensor]:
+        h_node = self.node_encoder(b, per_obs_no_mp, plan)
         h_dag = self.dag_encoder(h_node, b)
         return {"node": h_node, "dag": h_dag, "glob": self.global_encoder(h_dag, b)}
 
@@ -413,13 +488,17 @@ class StagePolicyNetwork(nn.Module):
         self.mlp_score = make_mlp(num_node_features + emb_dims["node"] + emb_dims["dag"] + emb_dims["glob"],
                                   output_dim=1, **mlp_kwargs)
 
-    def scores_all(self, b: DagBatch, h: dict[str, torch.Tensor], compact: bool = False) -> torch.Tensor:
+    def scores_all(self, b: DagBatch, h: dict[str, torch.Tensor], compact: bool = False,
+                   plan: LearnerPlan | None = None) -> torch.Tensor:
         """Score of every node row (only schedulable rows are meaningful). compact (the learner): the MLP runs on the
-        schedulable rows only, the others are 0."""
+        schedulable rows only, the others are 0 (their count from `plan` when given: no host sync)."""
         if not compact:
             inp = torch.cat([b.x, h["node"], h["dag"][b.node_dag], h["glob"][b.node_env]], dim=1)
             return self.mlp_score(inp).squeeze(-1)
-        idx = torch.nonzero(b.stage_mask).squeeze(1)
+        if plan is not None:
+            idx = torch.nonzero_static(b.stage_mask, size=plan.sched).squeeze(1)
+        else:
+            idx = torch.nonzero(b.stage_mask).squeeze(1)
         inp = torch.cat([b.x[idx], h["node"][idx], h["dag"][b.node_dag[idx]], h["glob"][b.node_env[idx]]], dim=1)
         out = torch.zeros(b.x.shape[0], dtype=h["node"].dtype, device=b.x.device)
         return out.index_put((idx,), self.mlp_score(inp).squeeze(-1))
@@ -589,13 +668,14 @@ class DecimaScheduler(nn.Module):
         return out
 
     def evaluate_actions(self, b: DagBatch, stage_idx: torch.Tensor, job_idx: torch.Tensor,
-                         exec_idx: torch.Tensor) -> dict[str, torch.Tensor]:
+                         exec_idx: torch.Tensor, plan: LearnerPlan | None = None) -> dict[str, torch.Tensor]:
         """scheduler.py:103-145 over a batch of observations (one per env row of `b`), with grads:
-        log-probabilities and normalised entropies of the given actions (utils.py:25-48, clamp_probs)."""
+        log-probabilities and normalised entropies of the given actions (utils.py:25-48, clamp_probs). `plan`
+        (minibatch_plans): the compact path's index-set sizes, so the forward issues no host sync."""
         B = b.num_envs
         dev = b.x.device
-        h = self.encoder(b, per_obs_no_mp=False)
-        scores = self.stage_policy_network.scores_all(b, h, compact=True)
+        h = self.encoder(b, per_obs_no_mp=False, plan=plan)
+        scores = self.stage_policy_network.scores_all(b, h, compact=True, plan=plan)
         probs, logp = masked_softmax_stats(scores, b.stage_mask, b.node_env, B, clamp=True)
         rows = torch.arange(b.x.shape[0], device=dev)
         hit = b.stage_mask & (self._sched_rows(b) == stage_idx.long()[b.node_env])

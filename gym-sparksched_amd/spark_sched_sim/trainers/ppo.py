@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from ..distributed import all_gather_var, gather_var, split_rows
-from ..schedulers.decima import DagBatch, DecimaScheduler, cat_batches, select_envs
+from ..schedulers.decima import DagBatch, DecimaScheduler, cat_batches, learner_counts, minibatch_plans, select_envs
 from .returns import Baseline, ReturnsCalculator
 from .rollouts import AsyncRolloutCollector, DeviceRolloutCollector, RolloutCollector
 
@@ -237,31 +237,39 @@ class PPO:
         return {"policy loss": v[0], "entropy": v[1], "approx kl div": v[2], "samples": int(v[3])}
 
     def _train(self, obs, acts, advg) -> dict[str, Any]:
+        """ppo.py:51-103. Host syncs: one per epoch for the sizes of all its minibatches (the index sets of the
+        compact learner path, minibatch_plans), and one per minibatch for the approx-KL early stop, whose value
+        decides whether the update runs (ppo.py:88-91); the losses are summed on the device."""
         n = obs.num_envs
         bs = n // self.num_batches + 1  # ppo.py:69
         pol_losses, ent_losses, kls = [], [], []
         cont = True
         self.scheduler.train()
+        counts = learner_counts(obs)
         for _ in range(self.num_epochs):
             if not cont:
                 break
             perm = torch.randperm(n, device=advg.device, generator=self.gen)  # DataLoader(shuffle=True)
-            for k in range(0, n, bs):
-                idx = perm[k: k + bs]
-                loss, info = self._loss(select_envs(obs, idx), {a: t[idx] for a, t in acts.items()}, advg[idx])
+            groups = [perm[k: k + bs] for k in range(0, n, bs)]
+            plans = minibatch_plans(obs, counts, groups)
+            for idx, (sizes, plan) in zip(groups, plans):
+                loss, info = self._loss(select_envs(obs, idx, sizes), {a: t[idx] for a, t in acts.items()}, advg[idx],
+                                        plan)
                 pol_losses.append(info["policy_loss"])
                 ent_losses.append(info["entropy_loss"])
-                kls.append(info["approx_kl_div"])
-                if self.target_kl is not None and info["approx_kl_div"] > 1.5 * self.target_kl:
+                kl = float(info["approx_kl_div"])
+                kls.append(kl)
+                if self.target_kl is not None and kl > 1.5 * self.target_kl:
                     cont = False  # ppo.py:88-91
                     break
                 self._update(loss)
-        return {"policy loss": abs(float(np.mean(pol_losses))), "entropy": abs(float(np.mean(ent_losses))),
-                "approx kl div": abs(float(np.mean(kls))), "samples": n}
+        pl = torch.stack(pol_losses).mean().item()
+        el = torch.stack(ent_losses).mean().item()
+        return {"policy loss": abs(pl), "entropy": abs(el), "approx kl div": abs(float(np.mean(kls))), "samples": n}
 
-    def _loss(self, obs, acts, advg):
-        """CLIP loss (ppo.py:105-138)."""
-        ev = self.scheduler.evaluate_actions(obs, acts["stage_idx"], acts["job_idx"], acts["exec_idx"])
+    def _loss(self, obs, acts, advg, plan=None):
+        """CLIP loss (ppo.py:105-138). The statistics stay device tensors (no host sync here)."""
+        ev = self.scheduler.evaluate_actions(obs, acts["stage_idx"], acts["job_idx"], acts["exec_idx"], plan=plan)
         a = (advg - advg.mean()) / (advg.std() + EPS)  # ppo.py:118-119
         log_ratio = ev["lgprobs"] - acts["lgprob"]
         ratio = log_ratio.exp()
@@ -270,8 +278,7 @@ class PPO:
         loss = pl + self.entropy_coeff * el
         with torch.no_grad():
             kl = ((ratio - 1) - log_ratio).mean()
-        return loss, {"policy_loss": float(pl.detach()), "entropy_loss": float(el.detach()),
-                      "approx_kl_div": float(kl)}
+        return loss, {"policy_loss": pl.detach(), "entropy_loss": el.detach(), "approx_kl_div": kl}
 
     def _update(self, loss):
         """TrainableScheduler.update_parameters (scheduler.py:34-53)."""

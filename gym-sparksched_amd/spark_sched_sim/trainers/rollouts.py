@@ -381,6 +381,11 @@ class DeviceRolloutCollector(RolloutCollector):
             if not (cur[:, _abi.CUR_FULL] != 0).any():
                 break
             self.arena.grow(cur)
+        err = eng.views["counts"][:, _abi.OC_ERR].cpu().numpy() & _abi.SSIM_ERR_STICKY
+        if err.any():  # e.g. an action the engine refused (frozen with SSIM_ERR_INVARIANT): its samples are invalid
+            bad = np.flatnonzero(err)
+            raise RuntimeError(f"decima rollout: envs {bad[:8].tolist()} frozen with error bits "
+                               f"{[hex(int(x)) for x in err[bad[:8]]]}")
         wall = eng.views["wall_time"].double().clone()
         return self.arena.buffer(wall)
 

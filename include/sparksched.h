@@ -305,6 +305,19 @@ int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t num_params,
 
 const char* ssim_last_error(void);
 
+/* Test hook, not part of the drop-in surface: a trace of CPython-set operations (add / remove / idle order) on one
+ * executor pool of env 0 through the engine's own set code, for known-answer tests against CPython
+ * (tests/test_gpu_sets.py). ops: device int32 [n_ops][6] = (code, key, busy bitmap words 0..3), code 0 add, 1 remove,
+ * 2 idle order (list(set(e for e in pool.copy() if not busy[e])), spark_sched_sim.py:714-728); orders: device int32
+ * [n_ops][width], the set's iteration order after codes 0/1 and the idle order for code 2, -1 padded. Clobbers env 0;
+ * needs 1..127 executors. */
+int ssim_debug_set_trace(ssim_handle* h, const int32_t* ops, int32_t n_ops, int32_t width, int32_t* orders,
+                         void* stream);
+
+/* Identity of this build: a hash of the library's kernel sources and compile definitions (__graft_entry__.build_lib).
+ * bench.py quotes PMC traffic only from a PMC summary (profiles/) made with the same build. */
+const char* ssim_build_id(void);
+
 #ifdef __cplusplus
 }
 #endif

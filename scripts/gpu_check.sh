@@ -21,6 +21,9 @@ for s in "$@"; do
     pytest)  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     pytestall) step pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread ;;
     pytestk) step pytest_k 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PYTEST_K" ;;
+    sets)    step pytest_sets 300 python -u -m pytest tests/test_gpu_sets.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
+    bench_large_nocpu) step bench_large_nocpu 300 python bench.py --workload large --steps 100 --warmup 20 --no-cpu-baseline ;;
+    bench_decima_nocpu) step bench_decima_nocpu 300 python bench.py --workload decima --steps 40 --warmup 5 --no-cpu-baseline ;;
     bench_driver) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     bench)   step bench 400 python bench.py ;;
     bench_nocpu) step bench_nocpu 300 python bench.py --no-cpu-baseline ;;

@@ -26,7 +26,7 @@ def main():
 
     lib = ct.CDLL(PP.build_prof())
     lib.ssim_rollout_budget_profiled.argtypes = [ct.c_void_p, ct.c_int32, ct.c_uint64, ct.c_int32, ct.c_int64,
-                                                 ct.c_int32, ct.c_void_p, ct.c_void_p]
+                                                 ct.c_int32, ct.c_void_p, ct.c_void_p, ct.c_void_p]
     native._lib = None
     native.LIB_PATH = os.path.join(REPO, "gym-sparksched_amd", "build", "libsparksched_prof.so")
     cfg = {"num_executors": 10, "job_arrival_cap": 50, "job_arrival_rate": 4.0e-5, "moving_delay": 2000.0,
@@ -50,7 +50,7 @@ def main():
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 ev[0].record()
                 lib.ssim_rollout_budget_profiled(eng.handle, _abi.SSIM_POLICY_RANDOM, 1234, 8 * k, B * k, flags,
-                                                 prof.data_ptr(), eng._stream())
+                                                 prof.data_ptr(), None, eng._stream())
                 ev[1].record()
                 torch.cuda.synchronize()
                 a1 = eng.views["acc"][:, _abi.ACC_DECISIONS].sum().item()

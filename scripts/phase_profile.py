@@ -48,34 +48,44 @@ def main():
     from spark_sched_sim import _abi, native
     from spark_sched_sim.data_samplers.synthetic_tpch import generate
 
-    cfg = {"num_executors": 10, "job_arrival_cap": 50, "job_arrival_rate": 4.0e-5, "moving_delay": 2000.0,
-           "warmup_delay": 1000.0}
+    import bench
+    from spark_sched_sim.wrappers import StochasticTimeLimitSampler
+
+    # PROF_WORKLOAD: one of bench.py's heuristic-policy workloads (tpch = configs[1], large = the configs[3] shard)
+    wl = bench.WORKLOADS[os.environ.get("PROF_WORKLOAD", "tpch")]
+    cfg = dict(wl["cfg"])
     ds = generate(int(os.environ.get("PROF_DATASET", "0")))
-    B = 1024
+    B = int(os.environ.get("PROF_ENVS", wl["envs"]))
+    limits = None
+    if wl["mean_time_limit"]:
+        smp = StochasticTimeLimitSampler(wl["mean_time_limit"], B, seed=42)
+        limits = np.array([smp.sample(i, i) for i in range(B)], dtype=np.float64)
     native._lib = None
     native.LIB_PATH = build_prof()
     from spark_sched_sim.engine import DeviceEngine
 
     lib = native.lib()
     lib.ssim_rollout_budget_profiled.argtypes = [ct.c_void_p, ct.c_int32, ct.c_uint64, ct.c_int32, ct.c_int64,
-                                                 ct.c_int32, ct.c_void_p, ct.c_void_p]
+                                                 ct.c_int32, ct.c_void_p, ct.c_void_p, ct.c_void_p]
     res = {}
     flags = _abi.SSIM_ROLLOUT_AUTORESET | _abi.SSIM_ROLLOUT_PREEMPT
     for K in [int(k) for k in os.environ.get("PROF_STEPS", "20,300").split(",")]:
         eng = DeviceEngine(cfg, B, ds)
-        eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=list(range(B)))
-        pre = np.random.default_rng([0, 0, 7]).integers(0, 1000, B).astype(np.int32)
+        eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=list(range(B)), time_limits=limits)
+        pre = np.random.default_rng([0, 0, 7]).integers(0, wl["preroll"], B).astype(np.int32)
         eng.rollout_steps(_abi.SSIM_POLICY_RANDOM, 4321, pre, int(pre.max()) + 1,
-                          flags=_abi.SSIM_ROLLOUT_AUTORESET | _abi.SSIM_ROLLOUT_WARMUP)
+                          flags=_abi.SSIM_ROLLOUT_AUTORESET | _abi.SSIM_ROLLOUT_WARMUP, time_limits=limits)
         for _ in range(int(os.environ.get("PROF_WARMUP", "5"))):
-            eng.rollout_budget(_abi.SSIM_POLICY_RANDOM, 1234, 8 * K, B * K, flags=flags | _abi.SSIM_ROLLOUT_WARMUP)
+            eng.rollout_budget(_abi.SSIM_POLICY_RANDOM, 1234, 8 * K, B * K, flags=flags | _abi.SSIM_ROLLOUT_WARMUP,
+                               time_limits=limits)
         torch.cuda.synchronize()
         acc = eng.views["acc"]
         d0 = acc[:, _abi.ACC_DECISIONS].sum().item()
         e0 = acc[:, 3].sum().item()
         prof = torch.zeros((B, NUM_SLOTS), dtype=torch.int64, device=eng.device)
+        tl = None if limits is None else torch.as_tensor(limits, device=eng.device)
         rc = lib.ssim_rollout_budget_profiled(eng.handle, _abi.SSIM_POLICY_RANDOM, 1234, 8 * K, B * K, flags,
-                                              prof.data_ptr(), eng._stream())
+                                              prof.data_ptr(), None if tl is None else tl.data_ptr(), eng._stream())
         native.check(rc, "ssim_rollout_budget_profiled")
         torch.cuda.synchronize()
         d1 = acc[:, _abi.ACC_DECISIONS].sum().item()

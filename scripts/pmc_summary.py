@@ -62,6 +62,9 @@ def main():
                 spl = cfg.get("steps_per_launch", b["steps"] if cfg["mode"] == "rollout" else 1)
                 dec = b["decisions"] * spl / b["steps"]  # launches are equal-length (bench --chunk)
             entry["kernel_name"] = name
+            if b and b.get("build_id"):  # every pass must have run the same library build
+                if entry.setdefault("build_id", b["build_id"]) != b["build_id"]:
+                    raise SystemExit(f"pass {pas} ran build {b['build_id']}, earlier passes {entry['build_id']}")
             entry.setdefault("decisions_per_dispatch", dec)
             entry.setdefault("config", b["config"] if b else None)
             entry.setdefault("steps", steps)

@@ -646,6 +646,53 @@ def replay_with_autoreset(cfg, dataset, seed, limit, actions, trace=False):
     return o, ob, ep, dec, last
 
 
+class _Replayed:
+    """What check_replayed_env reads of a replayed oracle (wall time, job times, trace), picklable for the pool."""
+
+    def __init__(self, o):
+        from types import SimpleNamespace
+
+        self.wall_time = o.wall_time
+        self.jobs = {jid: SimpleNamespace(t_arrival=j.t_arrival, t_completed=j.t_completed) for jid, j in o.jobs.items()}
+        self.trace = getattr(o, "trace", None)
+
+
+_POOL_DATASET = None
+
+
+def _pool_init(dataset):
+    global _POOL_DATASET
+    _POOL_DATASET = dataset
+
+
+def _replay_one(args):
+    cfg, seed, limit, actions, trace = args
+    o, ob, ep, dec, last = replay_with_autoreset(cfg, _POOL_DATASET, seed, limit, actions, trace=trace)
+    return _Replayed(o), ob, ep, dec, last
+
+
+def replay_many(cfg, dataset, items, trace=False):
+    """replay_with_autoreset for many envs, fanned out over the CPUs this job may use (spawn processes: the
+    parent holds a GPU context). items: (seed, limit, actions) per env. Returns (oracle view, obs, episodes,
+    decisions, last reward) per env, in order."""
+    import multiprocessing as mp
+
+    import bench
+
+    jobs = [(cfg, s, lim, a, trace) for s, lim, a in items]
+    procs = min(bench.usable_cpus(), 16, len(jobs))
+    if procs <= 1:
+        return [_replay_one_local(dataset, j) for j in jobs]
+    with mp.get_context("spawn").Pool(procs, initializer=_pool_init, initargs=(dataset,)) as pool:
+        return pool.map(_replay_one, jobs, chunksize=max(1, len(jobs) // (4 * procs)))
+
+
+def _replay_one_local(dataset, job):
+    cfg, seed, limit, actions, trace = job
+    o, ob, ep, dec, last = replay_with_autoreset(cfg, dataset, seed, limit, actions, trace=trace)
+    return o, ob, ep, dec, last
+
+
 def check_replayed_env(eng, v, ta, tc, i, o, ob, ep, dec, last, what, trace=False):
     c = v["counts"][i]
     assert int(c[_abi.OC_ERR]) == 0, f"{what} env{i} err {int(c[_abi.OC_ERR])}"
@@ -742,12 +789,12 @@ def case_bench_rollout_sequence(make, dataset, cfg, B, preroll, warmup, K, strid
     # every stride-th env, plus the first envs (up to 4 more) that went through an auto-reset
     multi = [int(i) for i in np.nonzero(v["counts"][:, _abi.OC_EPISODE] > 1)[0] if i % stride][:4]
     sample = sorted(set(range(0, B, stride)) | set(multi))
-    for i in sample:
-        o, ob, ep, dec, last = replay_with_autoreset(cfg, dataset, seeds[i], None if lim is None else lim[i],
-                                                     actions[i], trace=trace_cap > 0)
+    replays = replay_many(cfg, dataset, [(seeds[i], None if lim is None else lim[i], actions[i]) for i in sample],
+                          trace=trace_cap > 0)
+    for i, (o, ob, ep, dec, last) in zip(sample, replays):
         check_replayed_env(eng, v, ta, tc, i, o, ob, ep, dec, last, "bench-sequence", trace=trace_cap > 0)
         episodes += ep
         crossed += ep > 1
     return {"pending_at_timed_end": int(np.count_nonzero(pend)), "episodes_replayed": episodes,
-            "crossed_replayed": crossed, "decisions_replayed": int(applied[sample].sum()),
+            "crossed_replayed": crossed, "decisions_replayed": int(applied[sample].sum()), "envs_replayed": len(sample),
             "episodes_total": int(v["counts"][:, _abi.OC_EPISODE].sum())}

@@ -12,6 +12,20 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <stdint.h>
+
+// Diagnostic variant (-DSSIM_POOL_STATS, scripts/pool_stats.py): per CPython-set operation kind (add, remove,
+// idle order) a histogram over table sizes (log2) and the sum of the keys held.
+#ifdef SSIM_POOL_STATS
+static int64_t g_pool_ops[3][16], g_pool_keys[3][16];
+static inline void pool_stat(int op, int size, int used) {
+  int b = 0;
+  while ((1 << (b + 1)) <= size && b < 15) ++b;
+  g_pool_ops[op][b]++;
+  g_pool_keys[op][b] += used;
+}
+#define SSIM_POOL_STAT(op, size, used) pool_stat(op, size, used)
+#endif
 
 #include "decima.h"
 #include "engine.h"
@@ -240,6 +254,28 @@ int hs_decima(hs_handle* h, float nts, float ws, float* feats, int32_t* ccap, ui
   free(scratch);
   return 0;
 }
+
+// Per env: live stage window (live_hi - scan_live_lo), active stages, active jobs, arrived jobs.
+void hs_live_stats(hs_handle* h, int32_t* out) {
+  const Params* P = h->params;
+  for (int e = 0; e < P->L.num_envs; ++e) {
+    Sim<WaveSerial> s(P, h->state, h->scratch, h->obs, e, false);
+    s.load_header();
+    out[4 * e + 0] = s.live_hi() - s.scan_live_lo();
+    out[4 * e + 1] = s.h.n_active_stages;
+    out[4 * e + 2] = s.h.n_active_jobs;
+    out[4 * e + 3] = s.h.arrivals;
+  }
+}
+
+#ifdef SSIM_POOL_STATS
+void hs_pool_stats(int64_t* out) {  // [3][16] op counts then [3][16] key sums; resets the counters
+  memcpy(out, g_pool_ops, sizeof(g_pool_ops));
+  memcpy(out + 48, g_pool_keys, sizeof(g_pool_keys));
+  memset(g_pool_ops, 0, sizeof(g_pool_ops));
+  memset(g_pool_keys, 0, sizeof(g_pool_keys));
+}
+#endif
 
 // PCG64 / CPython-set models exposed for the known-answer tests.
 void hs_pcg_run(uint64_t* words, const int32_t* ops, int n_ops, double* out) {

@@ -36,6 +36,23 @@ def test_launcher_two_ranks_host_engine():
     assert line["decisions"] == 2 * B * K
     assert line["config"]["parallelism"] == "env-sharded x2"
     assert line["frozen_envs"] == 0 and line["roofline"] is None
+    # the process group held both ranks, and what each rank measured adds up to the reported total
+    assert line["ranks_seen"] == 2
+    assert sorted(r["rank"] for r in line["per_rank"]) == [0, 1]
+    assert sum(r["decisions"] for r in line["per_rank"]) == line["decisions"]
+    assert all(r["decisions"] == B * K for r in line["per_rank"])
+    assert max(r["elapsed_s"] for r in line["per_rank"]) <= line["ms_per_step"] * K / 1e3 + 1e-9
+
+
+def test_launcher_one_rank_reports_ranks_seen():
+    sys.path.insert(0, os.path.join(REPO, "tests", "hostsim"))
+    import driver
+
+    driver.build()
+    line = _run_bench("--engine", "host", "--steps", "3", "--warmup", "1", "--envs", "4", "--preroll", "20",
+                      "--no-cpu-baseline")
+    assert line["n_gpus"] == 1 and line["ranks_seen"] == 1
+    assert [r["rank"] for r in line["per_rank"]] == [0] and line["per_rank"][0]["decisions"] == line["decisions"]
 
 
 @pytest.mark.parametrize("workload", ["tpch", "decima"])

@@ -69,6 +69,44 @@ def test_registry_and_defaults(dataset):
     assert all(1 <= j.query_num <= 22 for _, j in seq)
 
 
+def test_custom_samplers_checked_at_registration(dataset):
+    """A plugin sampler must supply TPC-H-format tables (packed) and must not rely on a per-task task_duration hook
+    (data_sampler.py:19-23), which the device never calls: rejected with a clear TypeError when registered or built,
+    not at the first step. A sampler that only re-packages tables (e.g. a different job mix) is accepted."""
+    from spark_sched_sim.data_samplers import DataSampler, register_data_sampler
+    from spark_sched_sim.data_samplers import _REGISTRY
+
+    class ConstantDurations(SyntheticTPCHDataSampler):
+        def task_duration(self, job, stage, task, executor):
+            return 1000.0
+
+    with pytest.raises(TypeError, match="overrides task_duration"):
+        register_data_sampler(ConstantDurations)
+
+    class NoTables(DataSampler):
+        def job_sequence(self, max_time):
+            return []
+
+    with pytest.raises(TypeError, match="packed"):
+        register_data_sampler(NoTables)
+    _REGISTRY["ConstantDurations"] = ConstantDurations  # registered behind the check's back: caught at make time
+    try:
+        with pytest.raises(TypeError, match="overrides task_duration"):
+            make_data_sampler(dict(CFG, data_sampler_cls="ConstantDurations"))
+    finally:
+        del _REGISTRY["ConstantDurations"]
+
+    class SmallMix(SyntheticTPCHDataSampler):  # same tables and duration semantics: fine
+        pass
+
+    register_data_sampler(SmallMix)
+    try:
+        s = make_data_sampler(dict(CFG, data_sampler_cls="SmallMix", dataset="tpch"))
+        assert isinstance(s, SmallMix) and s.packed(10).num_templates > 0
+    finally:
+        del _REGISTRY["SmallMix"]
+
+
 def test_safe_loader_refuses_code(tmp_path):
     class Evil:
         def __reduce__(self):

@@ -113,6 +113,73 @@ def test_select_and_cat_batches_preserve_scores(dataset):
             assert torch.allclose(sc, torch.cat(alone), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_compact_encoder_equals_dense(dataset, seed):
+    """The learner's compact NodeEncoder (evaluate_actions: MLPs over leaves and each level's edge endpoints only)
+    against its dense form (force_dense: every row at every level) on batches of multi-level TPC-H observations:
+    node, DAG and global embeddings and the stage scores agree within float32 summation-order tolerance."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.schedulers.decima import DecimaScheduler, NodeEncoder, build_batch
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0)
+    eng = _host_engine(cfg, 8, dataset)
+    eng.reset(seeds=[100 * seed + i for i in range(8)])
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 11 + seed, 15 + 10 * seed)
+    v = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.host_views().items() if k != "trace"}
+    f = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.decima_features_np().items()}
+    b = build_batch(v, f)
+    assert b.max_levels >= 3, "needs observations with several message-passing levels"
+    torch.manual_seed(seed)
+    pol = DecimaScheduler(10)
+    with torch.no_grad():
+        compact = pol.encoder(b, per_obs_no_mp=False)
+        sc_compact = pol.stage_policy_network.scores_all(b, compact, compact=True)
+        try:
+            NodeEncoder.force_dense = True
+            dense = pol.encoder(b, per_obs_no_mp=False)
+        finally:
+            NodeEncoder.force_dense = False
+        sc_dense = pol.stage_policy_network.scores_all(b, dense)
+    for k in ("node", "dag", "glob"):
+        assert torch.allclose(compact[k], dense[k], rtol=1e-5, atol=1e-5), k
+    m = b.stage_mask
+    assert torch.allclose(sc_compact[m], sc_dense[m], rtol=1e-5, atol=1e-5)
+
+
+def test_minibatch_plans_match_sync_path(dataset):
+    """The PPO learner's minibatches with host-known index-set sizes (learner_counts / minibatch_plans: one sync per
+    epoch, nonzero_static inside the forward) give exactly the sub-batches and evaluate_actions outputs of the
+    per-call host-sync path (select_envs sizes via .tolist(), torch.nonzero / unique)."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.schedulers.decima import (DecimaScheduler, build_batch, learner_counts, minibatch_plans,
+                                                   select_envs)
+
+    cfg = dict(num_executors=10, job_arrival_cap=20, job_arrival_rate=4e-5, moving_delay=2000.0, warmup_delay=1000.0)
+    eng = _host_engine(cfg, 12, dataset)
+    eng.reset(seeds=[300 + i for i in range(12)])
+    eng.rollout(_abi.SSIM_POLICY_RANDOM, 9, 30)
+    v = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.host_views().items() if k != "trace"}
+    f = {k: torch.from_numpy(np.asarray(x)) for k, x in eng.decima_features_np().items()}
+    b = build_batch(v, f)
+    torch.manual_seed(3)
+    pol = DecimaScheduler(10)
+    gen = torch.Generator().manual_seed(1)
+    perm = torch.randperm(b.num_envs, generator=gen)
+    groups = [perm[k: k + 5] for k in range(0, b.num_envs, 5)]
+    plans = minibatch_plans(b, learner_counts(b), groups)
+    acts = pol.schedule(b)
+    for idx, (sizes, plan) in zip(groups, plans):
+        sub_sync, sub_plan = select_envs(b, idx), select_envs(b, idx, sizes)
+        for name in ("x", "edge_index", "edge_bits", "ptr", "node_dag", "node_env", "stage_mask"):
+            assert torch.equal(getattr(sub_sync, name), getattr(sub_plan, name)), name
+        assert (sub_sync.max_levels, sub_sync.max_nodes) == (sub_plan.max_levels, sub_plan.max_nodes)
+        args = (acts["stage_idx"][idx], acts["job_idx"][idx], acts["exec_idx"][idx])
+        with torch.no_grad():
+            a = pol.evaluate_actions(sub_sync, *args)
+            p = pol.evaluate_actions(sub_plan, *args, plan=plan)
+        assert torch.equal(a["lgprobs"], p["lgprobs"]) and torch.equal(a["entropies"], p["entropies"])
+
+
 def test_ppo_iteration_host(dataset):
     from spark_sched_sim.trainers import PPO
 
