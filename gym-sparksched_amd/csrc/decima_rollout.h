@@ -202,28 +202,29 @@ struct DecimaPolicy {
 #ifndef SSIM_DECIMA_ROLLOUT_WAVES
 #define SSIM_DECIMA_ROLLOUT_WAVES 4
 #endif
-template <bool kRes>
+// kN / kJ: executor count and job cap as compile-time constants (0 = read from the layout), as kernels.h.
+template <bool kRes, int kN, int kJ>
 __device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                     DecimaRolloutArgs a, int num_steps, int flags,
                                                     const double* __restrict__ limits, uint8_t* reset,
                                                     int32_t* action_log, int64_t budget, uint64_t* prof_out) {
   a.autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   const DecimaPolicy pol{P, obs, a};
-  rollout_body<kRes, 0, 0, 0>(P, state, obs, pol, num_steps, flags, limits, reset, action_log, prof_out, budget,
-                              nullptr);
+  rollout_body<kRes, kN, kJ, 0>(P, state, obs, pol, num_steps, flags, limits, reset, action_log, prof_out, budget,
+                                nullptr);
 }
-template <bool kRes>
+template <bool kRes, int kN = 0, int kJ = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_DECIMA_ROLLOUT_WAVES))) void k_decima_rollout(
     const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
     const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget, uint64_t* prof_out) {
-  decima_rollout_body<kRes>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
+  decima_rollout_body<kRes, kN, kJ>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
 }
 // launches that are not measured (SSIM_ROLLOUT_WARMUP), under their own symbol
-template <bool kRes>
+template <bool kRes, int kN = 0, int kJ = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_DECIMA_ROLLOUT_WAVES))) void k_decima_rollout_warmup(
     const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
     const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget, uint64_t* prof_out) {
-  decima_rollout_body<kRes>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
+  decima_rollout_body<kRes, kN, kJ>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
 }
 
 using DecimaRolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, DecimaRolloutArgs, int, int, const double*,
@@ -231,5 +232,6 @@ using DecimaRolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, DecimaRollou
 struct DecimaRolloutSet {
   DecimaRolloutFn rollout, rollout_warmup;
 };
-DecimaRolloutSet decima_rollout_hbm();  // k_dr_hbm.hip
-DecimaRolloutSet decima_rollout_lds();  // k_dr_lds.hip
+DecimaRolloutSet decima_rollout_hbm();    // k_dr_hbm.hip
+DecimaRolloutSet decima_rollout_hbm50();  // k_dr_hbm50.hip: 50 executors / 200 jobs
+DecimaRolloutSet decima_rollout_lds();    // k_dr_lds.hip

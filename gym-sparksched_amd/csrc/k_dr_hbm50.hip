@@ -1,0 +1,7 @@
+// k_dr_hbm50.hip — persistent Decima rollout (decima_rollout.h): hot block in HBM, specialised on the
+// config/decima_tpch.yaml env (50 executors / 200 jobs; configs[2]'s 4096 envs). One page of register event slots.
+#include "decima_rollout.h"
+
+DecimaRolloutSet decima_rollout_hbm50() {
+  return {k_decima_rollout<false, 50, 200>, k_decima_rollout_warmup<false, 50, 200>};
+}

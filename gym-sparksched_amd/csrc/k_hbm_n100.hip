@@ -1,0 +1,6 @@
+// k_hbm_n100.hip — step / rollout kernels: hot block in HBM, specialised on 100 executors / 200 jobs (the configs[3]
+// shard's shape; the stage cap is read at run time). Compile-time N and J fold the executor / job / commitment
+// section offsets and loop bounds into immediates, which takes SGPR pressure (and spills) off the 4-wave kernel.
+#include "kernels.h"
+
+KernelSet kernels_hbm_n100() { return kernel_set<false, 100, 200, 0>(); }

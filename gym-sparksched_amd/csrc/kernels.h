@@ -277,3 +277,5 @@ KernelSet kernels_bench900();  // k_bench900.hip: LDS-resident, 10 executors / 5
 KernelSet kernels_bench();     // k_bench.hip: LDS-resident, 10 executors / 50 jobs, stage cap at run time
 KernelSet kernels_lds();       // k_lds.hip: LDS-resident, any shape
 KernelSet kernels_hbm();       // k_hbm.hip: hot block in HBM, any shape
+KernelSet kernels_hbm_n100();  // k_hbm_n100.hip: hot block in HBM, 100 executors / 200 jobs (configs[3] shard)
+KernelSet kernels_hbm_n50();   // k_hbm_n50.hip: hot block in HBM, 50 executors / 200 jobs (decima_tpch.yaml env)

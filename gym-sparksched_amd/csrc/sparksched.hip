@@ -142,8 +142,13 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
 // on (executors, jobs) with the stage cap read at run time (any other TPC-H-format dataset, e.g. the real traces
 // loaded from data/tpch); other shapes use the generic instantiations.
 static bool bench_shape(const Params& p) { return p.L.num_executors == 10 && p.L.job_cap == 50; }
+static bool decima_shape(const Params& p) { return p.L.num_executors == 50 && p.L.job_cap == 200; }
 static KernelSet pick_kernels(const Params& p) {
-  if (!p.O.lds_resident) return kernels_hbm();
+  if (!p.O.lds_resident) {  // HBM-resident: the configs[2] / [3] shapes have (executors, jobs)-specialised kernels
+    if (p.L.num_executors == 100 && p.L.job_cap == 200) return kernels_hbm_n100();
+    if (decima_shape(p)) return kernels_hbm_n50();
+    return kernels_hbm();
+  }
   if (bench_shape(p)) return p.L.stage_cap == 900 ? kernels_bench900() : kernels_bench();
   return kernels_lds();
 }
@@ -554,7 +559,8 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
       return set_err(SSIM_E_ARG, "ssim_decima_rollout: incomplete sample arena");
     a.smp = sm;
   }
-  const DecimaRolloutSet ks = h->params.O.lds_resident ? decima_rollout_lds() : decima_rollout_hbm();
+  const DecimaRolloutSet ks = h->params.O.lds_resident ? decima_rollout_lds()
+                             : decima_shape(h->params) ? decima_rollout_hbm50() : decima_rollout_hbm();
   const DecimaRolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
   const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
   if (rc != SSIM_OK) return rc;
