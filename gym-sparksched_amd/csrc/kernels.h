@@ -9,6 +9,7 @@
 #include "sparksched.h"
 #include "engine.h"
 #include "policy.h"
+#include "rollout.h"
 #include "wave_hip.h"
 
 using namespace ssim;
@@ -33,6 +34,15 @@ __device__ __forceinline__ bool env_idle(const Params* __restrict__ P, const uin
 #endif
 #ifndef SSIM_HBM_STEP_WAVES
 #define SSIM_HBM_STEP_WAVES 4
+#endif
+// Waves per SIMD the windowed rollouts (kWS > 0) are compiled for: their LDS copy (~18 KB for a J = 200 env) lets
+// about two envs per SIMD share a CU, so they may use up to 256 VGPRs.
+#ifndef SSIM_WIN_WAVES
+#define SSIM_WIN_WAVES 2
+#endif
+// 1: a windowed rollout continues an env whose window outgrows the rings on the HBM-resident engine in the same wave
+#ifndef SSIM_WIN_FALLBACK
+#define SSIM_WIN_FALLBACK 1
 #endif
 constexpr int32_t kFlagTicketSlot = 0x100;  // internal k_rollout flag: use the second budget counter
 
@@ -94,28 +104,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
   s.save_hot();
 }
 
-// The action driver of a fused rollout: `act` chooses the next action of the env (false: the env takes no more
-// decisions in this launch, e.g. the Decima collector's episode ended or its sample arena is full), `done` runs after
-// a decision this launch started has completed (its observation written).
-struct HeuristicPolicy {  // fair / FIFO / random (policy.h)
-  int kind;
-  uint64_t seed;
-  // whether act() would choose an action (checked before a budget claim, so a claim is never spent on an env whose
-  // policy then declines)
-  template <class S>
-  __device__ __forceinline__ bool can_act(const S&) const {
-    return true;
-  }
-  template <class S>
-  __device__ __forceinline__ bool act(S& s, int /*k*/, StepIn* a) const {
-    *a = sim_policy(s, kind, seed);
-    return true;
-  }
-  template <class S>
-  __device__ __forceinline__ void done(S&) const {}
-};
-
-template <bool kRes, int kN, int kJ, int kS, class Pol>
+// kWS / kWJ > 0 (with kRes): the windowed engine (engine.h) runs the env from an LDS copy of its live window; an env
+// whose window does not fit the rings, at the launch's start or later, continues on the HBM-resident engine in the
+// same wave (both engines are inlined; the HBM path is the rare one).
+template <bool kRes, int kN, int kJ, int kS, class Pol, int kWS = 0, int kWJ = 0>
 __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                 const Pol& pol, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
@@ -133,18 +125,6 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
   }
   const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   if (!autoreset && action_log == nullptr && env_idle(P, state, eid)) return;
-#ifdef SSIM_PROFILE
-  const uint64_t rt_entry = WaveHip::realtime();
-#endif
-  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
-#ifdef SSIM_PROFILE
-  s.prof_set(kTCtor, WaveHip::realtime());
-#endif
-  s.load_hot();
-#ifdef SSIM_PROFILE
-  s.prof_set(kTEntry, rt_entry);
-  s.prof_set(kTLoaded, WaveHip::realtime());
-#endif
   // Shared budget (budget > 0): decisions are claimed from one device counter in chunks sized to what is
   // left (guided self-scheduling: 8 early, 1 at the end), so the launch ends within ~one decision of the
   // budget running out instead of waiting for the env with the most expensive K decisions. With
@@ -156,80 +136,67 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
   const int slot = (flags & kFlagTicketSlot) ? 1 : 0;
   const TicketStop stop{budget > 0 ? state + kTicketOffset + kTicketSlotBytes * slot : nullptr, budget,
                         eid % kStopLines, budget > 0 && (flags & SSIM_ROLLOUT_PREEMPT) != 0};
-  int64_t granted = 0, last = 0;
-  // One loop both starts steps and completes a step a previous launch preempted (pending), so the simulation /
-  // observation code (finish_step) is inlined once.
-  for (int k = 0;;) {
-#ifdef SSIM_PROFILE
-    const uint64_t t0 = WaveHip::clock();
-#endif
-    s.load_header();
-    // episode over (terminated, or truncated by the time limit): reset(seed=None) in place, before anything else
-    // (one call site for the whole loop). A preemptible budget launch resets only when it holds a claimed
-    // decision for the new episode: an episode that ends as the budget runs out is reset at the start of the
-    // env's next launch, so no wave spends the end of a launch on a reset.
-    if (autoreset && s.h.num_jobs > 0 && !s.frozen() && (s.h.terminated || s.h.wall >= s.h.time_limit) &&
-        !s.pending()) {  // (a step preempted past the time limit completes first)
-      if (stop.on && granted == 0 && (granted = stop.claim(B, last)) == 0) break;
-#ifdef SSIM_PROFILE
-      const uint64_t tr = WaveHip::clock();
-#endif
-      s.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limits != nullptr ? limits[eid] : __builtin_inf(),
-                      reset + (int64_t)eid * P->L.reset_stride);
-#ifdef SSIM_PROFILE
-      s.prof_add(kPhReset, WaveHip::clock() - tr);
-      s.prof_add(kCtReset, 1);
-#endif
-      continue;
+  RolloutCursor c{0, 0, 0};
+  const double limit = limits != nullptr ? limits[eid] : __builtin_inf();
+  uint8_t* rec = reset + (int64_t)eid * P->L.reset_stride;
+  if constexpr (kWS > 0) {
+    static_assert(kRes, "the windowed engine is LDS-resident");
+    Sim<WaveHip, kN, kJ, kS, kWS, kWJ> w(P, state, g_smem, obs, eid, true);
+    int why = kLoopReloadFailed;
+    if (w.load_window()) {
+      // an episode's reset runs on the home layout (HBM engine), then the window of the new episode is loaded
+      const auto reset_win = [&](Sim<WaveHip, kN, kJ, kS, kWS, kWJ>& x) {
+        x.save_window();
+        WaveHip::gsync();
+        {
+          Sim<WaveHip, kN, kJ, kS> r(P, state, g_smem, obs, eid, false);
+          r.load_header();
+          r.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limit, rec);
+        }
+        WaveHip::gsync();
+        return x.load_window();
+      };
+      why = rollout_loop(w, pol, stop, c, B, eid, num_steps, autoreset, action_log, reset_win);
+      if (why != kLoopReloadFailed) w.save_window();
     }
-    double st0 = 0.0;
-    bool simulate;
-    if (s.pending()) {  // completes first, whatever this launch's mode; not one of its num_steps
-      st0 = s.take_pending();
-      simulate = true;
-    } else {
-      if (k >= num_steps) break;
-      if (!pol.can_act(s)) break;
-      if (stop.base != nullptr) {
-        if (!autoreset && (s.h.terminated || s.frozen())) break;
-        if (granted == 0 && (granted = stop.claim(B, last)) == 0) break;
-        --granted;
-      }
-      StepIn a;
-      if (!pol.act(s, k, &a)) break;  // (never after can_act: a claimed decision is always taken)
-#ifdef SSIM_PROFILE
-      s.prof_add(kPhPolicy, WaveHip::clock() - t0);
-#endif
-      if (action_log != nullptr && WaveHip::lane() == 0) {
-        action_log[((int64_t)k * B + eid) * 2 + 0] = a.stage_idx;
-        action_log[((int64_t)k * B + eid) * 2 + 1] = a.num_exec;
-      }
-      ++k;
-      WaveHip::sync();
-      simulate = s.step_begin(a, &st0);
-      if (!simulate && s.rejected) {  // a device policy chose an invalid action: freeze the env (the host sees it)
-        s.fail(SSIM_ERR_INVARIANT);
-        s.store_header();
-        s.write_err_only(0u);
-        break;
-      }
-      if (!simulate) pol.done(s);
+    if (why == kLoopDone) {
+      if (c.granted > 0) stop.give_back(c.granted);
+      return;
     }
-    if (simulate) {
-      if (!s.finish_step(st0, stop)) break;  // preempted mid-simulation: pending until the next launch
-      pol.done(s);
-    }
-#ifdef SSIM_PROFILE
-    {
-      const uint64_t dc = WaveHip::clock() - t0;
-      int b = 63 - __builtin_clzll(dc | 1ull) - 10;
-      b = b < 0 ? 0 : b > 15 ? 15 : b;
-      s.prof_add(kHist0 + b, 1);
-      s.prof_add(kPhIter, dc);
+    WaveHip::gsync();  // the window's home copy before the HBM engine reads it
+#if !SSIM_WIN_FALLBACK
+    {  // (experiment builds without the HBM engine: the env freezes with a capacity error instead)
+      Sim<WaveHip, kN, kJ, kS> x(P, state, g_smem, obs, eid, false);
+      x.load_header();
+      x.fail(SSIM_ERR_CAPACITY);
+      x.store_header();
+      x.write_err_only(0u);
+      if (c.granted > 0) stop.give_back(c.granted);
+      return;
     }
 #endif
   }
-  if (granted > 0) stop.give_back(granted);  // a chunk the wave could not use (its step cap or episode end)
+  // HBM-resident (kRes false), LDS-resident with the whole hot block (kRes true, no window), or the windowed engine's
+  // fallback (kWS > 0: the hot block stays in HBM)
+  constexpr bool kResHere = kRes && kWS == 0;
+#ifdef SSIM_PROFILE
+  const uint64_t rt_entry = WaveHip::realtime();
+#endif
+  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kResHere);
+#ifdef SSIM_PROFILE
+  s.prof_set(kTCtor, WaveHip::realtime());
+#endif
+  s.load_hot();
+#ifdef SSIM_PROFILE
+  s.prof_set(kTEntry, rt_entry);
+  s.prof_set(kTLoaded, WaveHip::realtime());
+#endif
+  const auto reset_in_place = [&](Sim<WaveHip, kN, kJ, kS>& x) {
+    x.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limit, rec);
+    return true;
+  };
+  rollout_loop(s, pol, stop, c, B, eid, num_steps, autoreset, action_log, reset_in_place);
+  if (c.granted > 0) stop.give_back(c.granted);  // a chunk the wave could not use (its step cap or episode end)
 #ifdef SSIM_PROFILE
   s.prof_set(kTLoopEnd, WaveHip::realtime());
 #endif
@@ -248,17 +215,18 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
   const Params *__restrict__ P, uint8_t *state, uint8_t *obs, int kind, uint64_t seed, int num_steps, int flags, \
       const double *__restrict__ limits, uint8_t *reset, int32_t *action_log, uint64_t *prof_out, int64_t budget, \
       const int32_t *__restrict__ env_steps
-template <bool kRes, int kN, int kJ, int kS>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_ROLLOUT_WAVES))) void k_rollout(SSIM_ROLLOUT_ARGS) {
-  rollout_body<kRes, kN, kJ, kS>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags, limits, reset, action_log,
-                                 prof_out, budget, env_steps);
+#define SSIM_ROLLOUT_WAVES(kRes, kWS) ((kWS) > 0 ? SSIM_WIN_WAVES : (kRes) ? 1 : SSIM_HBM_ROLLOUT_WAVES)
+template <bool kRes, int kN, int kJ, int kS, int kWS = 0, int kWJ = 0>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_ROLLOUT_WAVES(kRes, kWS)))) void k_rollout(SSIM_ROLLOUT_ARGS) {
+  rollout_body<kRes, kN, kJ, kS, HeuristicPolicy, kWS, kWJ>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags,
+                                                            limits, reset, action_log, prof_out, budget, env_steps);
 }
 // The same rollout under its own symbol for launches that are not measured (SSIM_ROLLOUT_WARMUP: a benchmark's
 // pre-roll and warm-up), so a profiler's per-kernel statistics of k_rollout cover the timed launches only.
-template <bool kRes, int kN, int kJ, int kS>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(kRes ? 1 : SSIM_HBM_ROLLOUT_WAVES))) void k_rollout_warmup(SSIM_ROLLOUT_ARGS) {
-  rollout_body<kRes, kN, kJ, kS>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags, limits, reset, action_log,
-                                 prof_out, budget, env_steps);
+template <bool kRes, int kN, int kJ, int kS, int kWS = 0, int kWJ = 0>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_ROLLOUT_WAVES(kRes, kWS)))) void k_rollout_warmup(SSIM_ROLLOUT_ARGS) {
+  rollout_body<kRes, kN, kJ, kS, HeuristicPolicy, kWS, kWJ>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags,
+                                                            limits, reset, action_log, prof_out, budget, env_steps);
 }
 
 using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
@@ -267,10 +235,17 @@ using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int
 struct KernelSet {
   StepFn step;
   RolloutFn rollout, rollout_warmup;
+  int win_jobs = 0, win_stages = 0;  // windowed rollouts: ring sizes (0: the rollout's residency is the layout's)
 };
 template <bool kRes, int kN, int kJ, int kS>
 inline KernelSet kernel_set() {
   return {k_step<kRes, kN, kJ, kS>, k_rollout<kRes, kN, kJ, kS>, k_rollout_warmup<kRes, kN, kJ, kS>};
+}
+// HBM-resident steps, windowed rollouts (rings of kWS stages / kWJ jobs; layout.h window_lds_bytes)
+template <int kN, int kJ, int kS, int kWS, int kWJ>
+inline KernelSet kernel_set_windowed() {
+  return {k_step<false, kN, kJ, kS>, k_rollout<true, kN, kJ, kS, kWS, kWJ>, k_rollout_warmup<true, kN, kJ, kS, kWS, kWJ>,
+          kWJ, kWS};
 }
 // one per translation unit
 KernelSet kernels_bench900();  // k_bench900.hip: LDS-resident, 10 executors / 50 jobs / stage cap 900
@@ -279,3 +254,5 @@ KernelSet kernels_lds();       // k_lds.hip: LDS-resident, any shape
 KernelSet kernels_hbm();       // k_hbm.hip: hot block in HBM, any shape
 KernelSet kernels_hbm_n100();  // k_hbm_n100.hip: hot block in HBM, 100 executors / 200 jobs (configs[3] shard)
 KernelSet kernels_hbm_n50();   // k_hbm_n50.hip: hot block in HBM, 50 executors / 200 jobs (decima_tpch.yaml env)
+KernelSet kernels_win_n100();  // k_win_n100.hip: HBM-resident steps, windowed rollouts, 100 executors / 200 jobs
+KernelSet kernels_win_n50();   // k_win_n50.hip: HBM-resident steps, windowed rollouts, 50 executors / 200 jobs

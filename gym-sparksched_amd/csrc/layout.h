@@ -45,7 +45,8 @@ struct EnvHeader {
   int32_t trace_len;
   int32_t step_events;
   int32_t src_idx;        // obs source_job_idx at the last observation
-  int32_t pad[2];
+  int32_t err_line;       // engine.h line of the check that raised the first sticky error (diagnostic)
+  int32_t pad;
 };
 static_assert(sizeof(EnvHeader) % 16 == 0, "header must keep 16-B alignment");
 
@@ -77,7 +78,8 @@ struct JobRec {
   int16_t tpl, base, nst, nact;      // template, first env stage, #stages, #active stages
   int16_t sat, local, supply, state; // saturated count, |local_executors|, exec supply, 0/1/2
   int32_t arr_dec, done_dec;         // decision counter at arrival / completion (reward union)
-  int32_t pad[2];
+  int32_t pick;  // heuristics find_stage of the job at the last observation (packed min key, engine.h observe)
+  int32_t pad;
 };
 static_assert(sizeof(JobRec) == 32, "job record");
 
@@ -140,7 +142,7 @@ struct StateOffsets {
   int64_t hot_bytes, cold_bytes, scratch_bytes, env_bytes;
   int64_t lds_bytes;        // scratch (+ hot when LDS-resident); decided by compute_layout
   int32_t lds_resident, row_of_lds;  // row_of_lds: observe()'s stage -> row map in the LDS scratch (sc_row_of)
-  int64_t hdr, acc, jobs, jtimes, active_jobs, picks, execs, sel_list, commits, stages, pools, active_stages,
+  int64_t hdr, acc, jobs, jtimes, active_jobs, execs, sel_list, commits, stages, pools, active_stages,
       sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/, row_of /*cold int16[S]*/;
   int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
@@ -183,8 +185,6 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   o = align16(o + (int64_t)sizeof(JobTimes) * J);
   O.active_jobs = o;
   o = align16(o + 2 * J);
-  O.picks = o;  // int32 [J]: per job id, heuristics find_stage at the last observation (packed, see observe)
-  o = align16(o + 4 * J);
   O.execs = o;
   o = align16(o + (int64_t)sizeof(ExecRec) * N);
   O.sel_list = o;
@@ -237,6 +237,22 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   s = align16(O.sc_row_of + 2 * S);
   O.scratch_bytes = s;
   return O;
+}
+
+// The LDS image of WINDOWED residency (engine.h kWS / kWJ): the hot block's layout for a job cap of `wj` and a stage
+// cap of `ws` — the ring sizes — so its fixed sections line up with the home layout up to the job records and every
+// per-job / per-stage section holds one ring (pool records: COMMON, wj job pools, ws stage pools). Its scratch has a
+// ws-entry stage -> row map. (Its cold offsets are unused: the cold block stays at the home layout's.)
+constexpr StateOffsets window_offsets(int64_t N, int64_t wj, int64_t ws) { return state_offsets(N, wj, ws); }
+// Ring sizes of the windowed rollouts of the J = 200 shapes (configs[2] / [3]: live windows of tens of stages and a
+// handful of jobs, scripts/pool_stats.py; larger windows continue on the HBM-resident engine).
+constexpr int kWinStages = 128, kWinJobs = 32;
+// Dynamic LDS of a windowed rollout launch: the window image and its scratch, or the HBM-resident fallback's scratch
+// (which reuses the same LDS), whichever is larger.
+constexpr int64_t window_lds_bytes(int64_t N, int64_t J, int64_t S, int64_t wj, int64_t ws, bool row_of_lds) {
+  const StateOffsets W = window_offsets(N, wj, ws), H = state_offsets(N, J, S);
+  const int64_t win = W.hot_bytes + W.scratch_bytes, hbm = row_of_lds ? H.scratch_bytes : H.scratch_hbm_bytes;
+  return win > hbm ? win : hbm;
 }
 
 // Computes the public layout and the private offsets. Returns false on a bad / unsupported config.

@@ -144,15 +144,15 @@ struct PolicyView {
 
 // The fused rollout's policy input: the header (loaded) and the picks of the env's last observation
 // (Sim::observe), read from the hot block instead of the obs arena the same wave just wrote.
-template <class W, int kN, int kJ, int kS>
-__device__ __forceinline__ StepIn sim_policy(Sim<W, kN, kJ, kS>& s, int kind, uint64_t seed) {
+template <class SimT>
+__device__ __forceinline__ StepIn sim_policy(SimT& s, int kind, uint64_t seed) {
+  using W = typename SimT::WT;
   const int16_t* aj = s.template H<int16_t>(s.O.active_jobs);
-  const int32_t* picks = s.template H<int32_t>(s.O.picks);
   const uint64_t counter = (uint64_t)s.h.decisions + ((uint64_t)s.h.episode << 32);
   return policy_act<W>(
       kind, seed, counter, s.eid, s.NE, s.h.n_active_jobs, s.committable(), s.h.src_idx,
       [&](int k) {
-        const int key = picks[aj[k]];
+        const int key = s.job(aj[k]).pick;
         return key == 0x7FFFFFFF ? -1 : (key & 0xFFFF);
       },
       [&](int k) { return (int)s.job(aj[k]).supply; });

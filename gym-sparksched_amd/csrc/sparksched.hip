@@ -9,6 +9,7 @@
 //   k_rollout : `num_steps` x (policy -> step) fused into one launch (no host round trips)
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+#include <stdlib.h>
 
 #include <mutex>
 #include <stdio.h>
@@ -143,9 +144,36 @@ __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, 
 // loaded from data/tpch); other shapes use the generic instantiations.
 static bool bench_shape(const Params& p) { return p.L.num_executors == 10 && p.L.job_cap == 50; }
 static bool decima_shape(const Params& p) { return p.L.num_executors == 50 && p.L.job_cap == 200; }
+static bool large_shape(const Params& p) { return p.L.num_executors == 100 && p.L.job_cap == 200; }
+// Diagnostic switch: SSIM_GENERIC=1 runs every HBM-resident layout on the generic (run-time shape) kernels.
+static bool generic_forced() {
+  static const int on = [] {
+    const char* v = getenv("SSIM_GENERIC");
+    return (v != nullptr && v[0] == '1') ? 1 : 0;
+  }();
+  return on != 0;
+}
+#if SSIM_WITH_WINDOWED
+// Experiment builds with the windowed rollouts (k_win_*.hip, k_dr_win50.hip): SSIM_WINDOW=1 selects them for the
+// configs[2] / [3] shapes.
+static bool windowed_enabled() {
+  static const int on = [] {
+    const char* v = getenv("SSIM_WINDOW");
+    return (v != nullptr && v[0] == '1') ? 1 : 0;
+  }();
+  return on != 0;
+}
+#else
+static bool windowed_enabled() { return false; }
+#endif
 static KernelSet pick_kernels(const Params& p) {
   if (!p.O.lds_resident) {  // HBM-resident: the configs[2] / [3] shapes have (executors, jobs)-specialised kernels
-    if (p.L.num_executors == 100 && p.L.job_cap == 200) return kernels_hbm_n100();
+    if (generic_forced()) return kernels_hbm();
+#if SSIM_WITH_WINDOWED
+    if (windowed_enabled() && large_shape(p)) return kernels_win_n100();
+    if (windowed_enabled() && decima_shape(p)) return kernels_win_n50();
+#endif
+    if (large_shape(p)) return kernels_hbm_n100();
     if (decima_shape(p)) return kernels_hbm_n50();
     return kernels_hbm();
   }
@@ -156,6 +184,12 @@ static StepFn pick_step(const Params& p) { return pick_kernels(p).step; }
 static RolloutFn pick_rollout(const Params& p, bool warmup = false) {
   const KernelSet k = pick_kernels(p);
   return warmup ? k.rollout_warmup : k.rollout;
+}
+// Dynamic LDS of a rollout launch: the layout's, or a windowed rollout's (window image + scratch, or the HBM
+// fallback's scratch)
+static int64_t rollout_lds(const Params& p, int win_jobs, int win_stages) {
+  if (win_stages == 0) return p.O.lds_bytes;
+  return window_lds_bytes(p.L.num_executors, p.L.job_cap, p.L.stage_cap, win_jobs, win_stages, p.O.row_of_lds != 0);
 }
 
 // ------------------------------------------------------------------------------------------ C ABI
@@ -341,14 +375,16 @@ static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t n
   if ((flags & SSIM_ROLLOUT_AUTORESET) && !(h->params.C.job_arrival_gap > 0.0))
     return set_err(SSIM_E_ARG, "ssim_rollout_ex: auto-reset needs job_arrival_gap in the config");
   const ssim_layout& L = h->params.L;
-  const RolloutFn fn = pick_rollout(h->params, (flags & SSIM_ROLLOUT_WARMUP) != 0);
-  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  const KernelSet ks = pick_kernels(h->params);
+  const RolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
+  const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   // the budget slot this launch claims from; flipped only once the launch is enqueued (a failed launch leaves the
   // slot it would have zeroed dirty, so the next launch must use the same one again)
   if (budget > 0 && h->ticket_slot) flags |= kFlagTicketSlot;
   hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64),
-                     (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+                     (size_t)lds, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, flags, time_limits, h->reset, action_log,
                      (uint64_t*)nullptr, budget, env_steps);
   const int rc2 = hip_check(hipGetLastError(), "k_rollout launch");
@@ -396,10 +432,12 @@ extern "C" int ssim_reset_sampled(ssim_handle* h, const uint8_t* mode, const uin
 extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
                                      uint64_t* prof_out, void* stream) {
   const ssim_layout& L = h->params.L;
-  const RolloutFn fn = pick_rollout(h->params);
-  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  const KernelSet ks = pick_kernels(h->params);
+  const RolloutFn fn = ks.rollout;
+  const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
-  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, num_steps, 0, (const double*)nullptr, h->reset,
                      (int32_t*)nullptr, prof_out, (int64_t)0, (const int32_t*)nullptr);
   return hip_check(hipGetLastError(), "k_rollout(profiled) launch");
@@ -410,11 +448,13 @@ extern "C" int ssim_rollout_budget_profiled(ssim_handle* h, int32_t kind, uint64
                                             const double* time_limits, void* stream) {
   const ssim_layout& L = h->params.L;
   if (total_decisions <= 0) return set_err(SSIM_E_ARG, "ssim_rollout_budget_profiled: total_decisions must be > 0");
-  const RolloutFn fn = pick_rollout(h->params);
-  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  const KernelSet ks = pick_kernels(h->params);
+  const RolloutFn fn = ks.rollout;
+  const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   if (h->ticket_slot) flags |= kFlagTicketSlot;
-  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream,
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream,
                      dparams(h), h->state, h->obs, kind, seed, max_steps, flags, time_limits, h->reset,
                      (int32_t*)nullptr, prof_out, total_decisions, (const int32_t*)nullptr);
   const int rc2 = hip_check(hipGetLastError(), "k_rollout(budget, profiled) launch");
@@ -559,13 +599,18 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
       return set_err(SSIM_E_ARG, "ssim_decima_rollout: incomplete sample arena");
     a.smp = sm;
   }
-  const DecimaRolloutSet ks = h->params.O.lds_resident ? decima_rollout_lds()
-                             : decima_shape(h->params) ? decima_rollout_hbm50() : decima_rollout_hbm();
+  DecimaRolloutSet ks = h->params.O.lds_resident   ? decima_rollout_lds()
+                       : !decima_shape(h->params) || generic_forced() ? decima_rollout_hbm()
+                                                  : decima_rollout_hbm50();
+#if SSIM_WITH_WINDOWED
+  if (!h->params.O.lds_resident && decima_shape(h->params) && windowed_enabled()) ks = decima_rollout_win50();
+#endif
   const DecimaRolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
-  const int rc = lds_opt_in((const void*)fn, h->params.O.lds_bytes);
+  const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   if (total_decisions > 0 && h->ticket_slot) flags |= kFlagTicketSlot;
-  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)h->params.O.lds_bytes, (hipStream_t)stream, dparams(h),
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream, dparams(h),
                      h->state, h->obs, a, max_steps, flags, time_limits, h->reset, action_log, total_decisions,
                      h->prof_next);
   h->prof_next = nullptr;

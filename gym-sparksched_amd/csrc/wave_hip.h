@@ -42,6 +42,13 @@ struct WaveHip {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
+  // Drains every outstanding memory operation of the wave (s_waitcnt 0). Lane-parallel scratch traffic whose stores,
+  // atomics and loads may be issued as different instruction kinds (FLAT through the texture path, DS direct to the
+  // LDS: not ordered against each other) is fenced with it before the data is read back.
+  __device__ static __forceinline__ void drain() {
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  }
   __device__ static __forceinline__ void gsync() {  // global-memory ordering across the wave's lanes
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();

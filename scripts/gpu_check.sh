@@ -6,6 +6,11 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p "$OUT"
+# heartbeat: a step that runs minutes without printing (a test fanning the oracle replay out over the CPUs) is not
+# hung; each step still has its own time limit below
+( while sleep 50; do date +%T >> "$OUT/heartbeat.log"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 step() {
   local name=$1 secs=$2; shift 2
   echo "=== $name ($(date +%T))"
@@ -21,6 +26,7 @@ for s in "$@"; do
     pytest)  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     pytestall) step pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread ;;
     pytestk) step pytest_k 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PYTEST_K" ;;
+    diag)    step diag_plain 240 env SSIM_WINDOW=0 python -u scripts/diag_large.py 64,20,0 4096,10,0 4096,5,8000 && step diag_win 240 python -u scripts/diag_large.py 64,20,0 4096,10,0 4096,5,8000 ;;
     sets)    step pytest_sets 300 python -u -m pytest tests/test_gpu_sets.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
     bench_large_nocpu) step bench_large_nocpu 300 python bench.py --workload large --steps 100 --warmup 20 --no-cpu-baseline ;;
     bench_decima_nocpu) step bench_decima_nocpu 300 python bench.py --workload decima --steps 40 --warmup 5 --no-cpu-baseline ;;
@@ -37,6 +43,7 @@ for s in "$@"; do
     prof)    step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     phase)   step phase 600 python scripts/phase_profile.py ;;
     sweep)   step sweep 900 bash scripts/steps_sweep.sh ;;
+    env_sweep) step env_sweep 1000 bash scripts/env_sweep.sh ;;
     ab)      step ab 900 bash scripts/ab_tpch.sh ;;
     ab_hbm)  step ab_hbm 1200 bash scripts/ab_hbm.sh ;;
     cpubase) step cpubase 900 python scripts/cpu_baselines.py ;;

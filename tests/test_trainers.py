@@ -609,3 +609,45 @@ def test_decima_rollout_preempted_collection_equals_one_launch(gpu_device, datas
         assert torch.equal(a.nodes[i, :nn], b.nodes[i, :nn]), f"env {i} nodes"
         assert torch.equal(a.edges[i, :ne], b.edges[i, :ne]), f"env {i} edges"
         assert torch.equal(a.dags[i, :nd], b.dags[i, :nd]), f"env {i} dags"
+
+
+@pytest.mark.gpu
+def test_decima_budget_not_spent_on_truncated_envs(gpu_device, dataset):
+    """A budgeted Decima collection (no auto-reset) where most envs are truncated by their time limit: the
+    policy's stop conditions are checked before a decision is claimed from the shared budget (DecimaPolicy::can_act),
+    so the truncated envs claim nothing and every launch's whole budget goes to the live envs (each launch adds
+    exactly `budget` samples while they have work)."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.engine import DeviceEngine
+    from spark_sched_sim.schedulers.decima import DecimaScheduler
+    from spark_sched_sim.trainers import DECIMA_TPCH
+    from spark_sched_sim.trainers.rollouts import DecimaSampleArena
+
+    env = {k: v for k, v in DECIMA_TPCH["env"].items() if k not in ("mean_time_limit", "dataset")}
+    B, live, budget = 16, 2, 16
+    limits = np.full(B, 1.0)  # truncated after the first decision moves the clock past 1 ms
+    limits[:live] = np.inf
+    torch.manual_seed(5)
+    pol = DecimaScheduler(env["num_executors"]).to(gpu_device)
+    params = pol.packed_params(gpu_device)
+    eng = DeviceEngine(env, B, dataset, device=gpu_device)
+    eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=[401 + i for i in range(B)], time_limits=limits)
+    arena = DecimaSampleArena(B, eng.device, cap_samples=256, cap_nodes=1 << 15, cap_edges=1 << 15, cap_dags=1 << 12)
+    added, counts = [], []
+    prev = 0
+    for _ in range(12):
+        eng.decima_rollout(params, 9, 77, 64, budget, flags=_abi.SSIM_ROLLOUT_PREEMPT, samples=arena)
+        cur = arena.cursor.cpu().numpy()
+        assert not (cur[:, _abi.CUR_FULL] != 0).any()
+        n = int(cur[:, 0].sum())
+        added.append(n - prev)
+        counts.append(cur[:, 0].copy())
+        prev = n
+    # the short-limit envs take the decisions of their first instants (several decisions at wall time 0), then
+    # pass their limit and stop
+    wall = eng.views["wall_time"].cpu().numpy()
+    assert (wall[live:] >= 1.0).all(), wall
+    last = max(k for k in range(len(counts)) if k == 0 or (counts[k][live:] != counts[k - 1][live:]).any())
+    assert last <= 6, (last, [c.tolist() for c in counts])
+    # from then on every launch's whole budget went to the live envs
+    assert added[last + 1:] == [budget] * (len(added) - last - 1), added
