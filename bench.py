@@ -362,6 +362,9 @@ def main():
                     help="rollout mode: budget launches finish every started step (no SSIM_ROLLOUT_PREEMPT)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="rollout mode: leave finished envs idle instead of resetting them on the device")
+    ap.add_argument("--force-hbm", action="store_true",
+                    help="diagnostic: keep the hot blocks in HBM (SSIM_CFG_FORCE_HBM) whatever their size: the "
+                         "HBM-resident kernels (4 waves per SIMD) instead of the LDS-resident one")
     ap.add_argument("--engine", choices=["hip", "host"], default="hip",
                     help="host = the TEST-ONLY CPU build of the engine (tests/hostsim) over gloo, to exercise the "
                          "launcher and the rank plumbing in the CPU test suite; never a measurement")
@@ -418,7 +421,8 @@ def main():
     else:
         from spark_sched_sim.engine import DeviceEngine
 
-        eng = DeviceEngine(cfg, B, generate(args.dataset_seed), device=dev)
+        eng = DeviceEngine(cfg, B, generate(args.dataset_seed), device=dev,
+                           config_flags=_abi.SSIM_CFG_FORCE_HBM if args.force_hbm else 0)
     seeds = shard_seeds(rank, B, args.seed)
     limits = None
     if wl["mean_time_limit"]:  # StochasticTimeLimit (wrappers/stochastic_time_limit.py:5-31), per env
@@ -606,6 +610,7 @@ def main():
                        "preroll": {"bound": preroll, "mean_decisions": float(pre_steps.mean())},
                        "autoreset": bool(mode != "step" and (flags or mode == "decima")),
                        "parallelism": f"env-sharded x{world}",
+                       "residency": "LDS" if int(eng.layout.lds_resident) else "HBM",
                        "dataset": {"generator": "synthetic_tpch", "seed": args.dataset_seed,
                                    "stage_cap": int(eng.layout.stage_cap),
                                    "kernel": ("shape-specialised (stage cap 900)" if int(eng.layout.stage_cap) == 900

@@ -705,10 +705,16 @@ struct Sim {
     if (W::lane() == 0) *H<EnvHeader>(O.hdr) = h;
     W::sync();
   }
-  // The first sticky error also records the engine.h source line that raised it (EnvHeader::err_line, a diagnostic
-  // for the host: which invariant or capacity check froze the env).
+  // Diagnostic builds (-DSSIM_ERR_LINE=1) also record the engine.h source line of the first sticky error
+  // (EnvHeader::err_line: which invariant or capacity check froze the env; scripts/diag_large.py). Off in the product
+  // build: the line select at every check site kept one more SGPR live through the engine (+51 SGPR spills on the
+  // bench kernel, -4.8% decisions/s).
   __device__ __forceinline__ void fail(uint32_t bits, int line = __builtin_LINE()) {
+#if SSIM_ERR_LINE
     if (!frozen() && (bits & SSIM_ERR_STICKY)) h.err_line = line;
+#else
+    (void)line;
+#endif
     h.err |= bits;
   }
   __device__ __forceinline__ bool frozen() const { return (h.err & SSIM_ERR_STICKY) != 0u; }

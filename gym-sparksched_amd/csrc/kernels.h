@@ -253,6 +253,7 @@ KernelSet kernels_bench();     // k_bench.hip: LDS-resident, 10 executors / 50 j
 KernelSet kernels_lds();       // k_lds.hip: LDS-resident, any shape
 KernelSet kernels_hbm();       // k_hbm.hip: hot block in HBM, any shape
 KernelSet kernels_hbm_n100();  // k_hbm_n100.hip: hot block in HBM, 100 executors / 200 jobs (configs[3] shard)
+KernelSet kernels_hbm_n10();   // k_hbm_n10.hip: hot block in HBM, 10 executors / 50 jobs (configs[1] env, large batches)
 KernelSet kernels_hbm_n50();   // k_hbm_n50.hip: hot block in HBM, 50 executors / 200 jobs (decima_tpch.yaml env)
 KernelSet kernels_win_n100();  // k_win_n100.hip: HBM-resident steps, windowed rollouts, 100 executors / 200 jobs
 KernelSet kernels_win_n50();   // k_win_n50.hip: HBM-resident steps, windowed rollouts, 50 executors / 200 jobs

@@ -123,6 +123,17 @@ constexpr int64_t kHbmWorkgroupsPerCu = 16;   // HBM-resident engine kernels: 4 
 // decima_tpch.yaml PPO iteration, whose J=200 / N=50 hot block (~146 KB) otherwise stays in HBM.
 constexpr int64_t kLdsBudgetBig = 160 * 1024;
 constexpr int64_t kBigLdsMaxEnvs = 256;
+// Batches past what the LDS-resident kernels hold at once. Those run one wave per SIMD (one env per wave, its hot
+// block in LDS: the configs[1] env's 40 KB lets 4 share a CU, 1024 on the chip's 256 CUs); a larger batch waits in
+// rounds, while the HBM-resident kernels keep 4 waves per SIMD in flight and hide the memory latency the LDS saves.
+// Measured on configs[1]'s env (profiles/r04/env_sweep_residency.log): LDS 3.55e7 decisions/s at every batch size
+// from 1024 to 8192 envs; HBM-resident (10, 50)-specialised kernels 1.5e7 at 1024, 4.0e7 at 2048, 5.2e7 at 3072,
+// 6.2e7 from 4096. So a batch above 1.5x the LDS-resident concurrency runs HBM-resident.
+constexpr int64_t kChipCus = 256;  // MI355X
+constexpr int64_t lds_concurrent_envs(int64_t need) {
+  const int64_t per_cu = kLdsPerCu / (need > 0 ? need : 1);
+  return kChipCus * (per_cu < 4 ? per_cu : 4);
+}
 
 struct TraceRec {  // one popped event
   double t;
@@ -282,7 +293,9 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
   L->scratch_bytes = O->scratch_bytes;
   // LDS per wave: [hot copy (if resident) | scratch]
   const int64_t need = O->hot_bytes + O->scratch_bytes;
-  O->lds_resident = (!(cfg.flags & SSIM_CFG_FORCE_HBM) && (need <= kLdsBudget || (need <= kLdsBudgetBig && B <= kBigLdsMaxEnvs)))
+  O->lds_resident = (!(cfg.flags & SSIM_CFG_FORCE_HBM) &&
+                     ((need <= kLdsBudget && 2 * B <= 3 * lds_concurrent_envs(need)) ||
+                      (need <= kLdsBudgetBig && B <= kBigLdsMaxEnvs)))
                         ? 1 : 0;
   L->lds_resident = O->lds_resident;
   // An HBM-resident kernel (4 waves per SIMD: 16 workgroups per CU) whose full scratch would not let 16 workgroups

@@ -175,6 +175,7 @@ static KernelSet pick_kernels(const Params& p) {
 #endif
     if (large_shape(p)) return kernels_hbm_n100();
     if (decima_shape(p)) return kernels_hbm_n50();
+    if (bench_shape(p)) return kernels_hbm_n10();
     return kernels_hbm();
   }
   if (bench_shape(p)) return p.L.stage_cap == 900 ? kernels_bench900() : kernels_bench();

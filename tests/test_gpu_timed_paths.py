@@ -42,6 +42,16 @@ def test_bench_tpch_timed_launch_replay(make, dataset, K, warmup, stride):
     assert r["crossed_replayed"] >= 1  # replayed envs crossed episode boundaries (auto-resets inside the sequence)
 
 
+def test_bench_tpch_large_batch_hbm_replay(make, dataset):
+    """configs[1]'s env at 4096 envs per GPU (`bench.py --envs 4096`): a batch past 1.5x what the LDS-resident kernel
+    holds at once runs on the HBM-resident (10 executors, 50 jobs)-specialised kernels (layout.h lds_concurrent_envs,
+    k_hbm_n10.hip). bench.py's 300-step sequence; every 64th env replayed on the oracle."""
+    r = cases.case_bench_rollout_sequence(make, dataset, TPCH, B=4096, preroll=1000, warmup=50, K=300, stride=64,
+                                          expect_resident=False)
+    assert r["envs_replayed"] >= 4096 // 64
+    assert r["crossed_replayed"] >= 1
+
+
 def test_bench_tpch_timed_launch_replay_traced(make, dataset):
     """The same sequence with event tracing on (trace records are written by a uniform branch the bench skips): the
     replayed envs' current-episode event traces (event order, executors, stage / job completions) bit for bit."""

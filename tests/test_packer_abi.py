@@ -124,6 +124,14 @@ def test_layout_structs_match_header():
         assert lib.ssim_layout_for(ctypes.byref(big), ctypes.byref(L)) == 0
         assert L.lds_resident == 0 and 16 * L.lds_bytes <= 160 * 1024, (n_exec, L.lds_bytes)
         assert (L.lds_bytes == L.scratch_bytes) == row_map_in_lds, (n_exec, L.lds_bytes, L.scratch_bytes)
+    # batches past 1.5x the LDS-resident kernel's concurrency (4 configs[1] envs per CU, 1024 on the chip) run on
+    # the 4-wave HBM-resident kernels (layout.h lds_concurrent_envs)
+    for envs, resident in ((1024, 1), (1536, 1), (1537, 0), (4096, 0)):
+        cfg.num_envs = envs
+        assert lib.ssim_layout_for(ctypes.byref(cfg), ctypes.byref(L)) == 0
+        assert L.lds_resident == resident, (envs, L.lds_resident)
+        if not resident:
+            assert 16 * L.lds_bytes <= 160 * 1024, L.lds_bytes
     cfg.num_executors = 0
     assert lib.ssim_layout_for(ctypes.byref(cfg), ctypes.byref(L)) != 0
 
