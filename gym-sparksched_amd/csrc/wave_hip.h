@@ -27,6 +27,13 @@ struct WaveHip {
     return ((uint64_t)hi << 32) | lo;
   }
   __device__ static __forceinline__ int64_t uni(int64_t v) { return (int64_t)uni((uint64_t)v); }
+  __device__ static __forceinline__ float uni(float v) {
+    return __builtin_bit_cast(float, uni(__builtin_bit_cast(uint32_t, v)));
+  }
+  template <class T>
+  __device__ static __forceinline__ T* uni(T* p) {
+    return reinterpret_cast<T*>(uni(reinterpret_cast<uint64_t>(p)));
+  }
   __device__ static __forceinline__ double uni(double v) {
     return __builtin_bit_cast(double, uni(__builtin_bit_cast(uint64_t, v)));
   }
