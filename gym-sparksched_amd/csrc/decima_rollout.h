@@ -74,7 +74,12 @@ struct DecimaPolicy {
         W::uni(cur[2]) + W::uni(cnt[SSIM_OC_NUM_EDGES]) > sm.cap_edges ||
         W::uni(cur[3]) + W::uni(cnt[SSIM_OC_NUM_JOBS]) > sm.cap_dags) {
       W::sync();
-      if (W::lane() == 0) cur[4] = 1;  // region full: the host grows the arena and launches again
+      if (W::lane() == 0) {  // region full: the host grows the arena (to fit what is recorded here), launches again
+        cur[4] = 1;
+        cur[5] = W::uni(cnt[SSIM_OC_NUM_NODES]);
+        cur[6] = W::uni(cnt[SSIM_OC_NUM_EDGES]);
+        cur[7] = W::uni(cnt[SSIM_OC_NUM_JOBS]);
+      }
       W::sync();
       return false;
     }

@@ -118,7 +118,7 @@ SAMPLE_BYTES = 64
 SAMPLE_LGPROB = 11  # float32 word index
 SAMPLE_WALL, SAMPLE_REWARD = 6, 7  # float64 word indices
 CURSOR_WORDS = 8
-CUR_SAMPLES, CUR_NODES, CUR_EDGES, CUR_DAGS, CUR_FULL = range(5)
+CUR_SAMPLES, CUR_NODES, CUR_EDGES, CUR_DAGS, CUR_FULL, CUR_NEED_NODES, CUR_NEED_EDGES, CUR_NEED_DAGS = range(8)
 
 
 def layout_dict(layout: SsimLayout) -> dict:

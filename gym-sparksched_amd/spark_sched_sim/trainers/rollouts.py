@@ -242,19 +242,26 @@ class DecimaSampleArena:
         out[:, : t.shape[1]] = t
         return out
 
+    @staticmethod
+    def required(cur: np.ndarray) -> list[int]:
+        """Per region (samples, node rows, edge rows, DAG rows): what the full envs' stopped observations need, i.e.
+        the rows used plus the rows the kernel recorded for the observation that did not fit (cursor[5..7])."""
+        f = cur[cur[:, _abi.CUR_FULL] != 0]
+        need = [f[:, _abi.CUR_SAMPLES] + 1, f[:, _abi.CUR_NODES] + f[:, _abi.CUR_NEED_NODES],
+                f[:, _abi.CUR_EDGES] + f[:, _abi.CUR_NEED_EDGES], f[:, _abi.CUR_DAGS] + f[:, _abi.CUR_NEED_DAGS]]
+        return [int(n.max()) if len(n) else 0 for n in need]
+
     def grow(self, cur: np.ndarray) -> None:
-        """After a launch that left envs with the full flag: double the regions that are >= 3/4 used by a full env
-        (all of them if none is), then clear the flags."""
-        full = cur[:, _abi.CUR_FULL] != 0
-        used = cur[full][:, [_abi.CUR_SAMPLES, _abi.CUR_NODES, _abi.CUR_EDGES, _abi.CUR_DAGS]].max(axis=0)
-        big = [u * 4 >= 3 * c for u, c in zip(used, self.caps)]
-        if not any(big):
-            big = [True] * 4
+        """After a launch that left envs with the full flag: every region a stopped observation overflows is grown
+        (doubling until it fits) so the next launch records it, then the flags are cleared."""
         names = ["rec", "nodes", "edges", "dags"]
-        for i, b in enumerate(big):
-            if b:
-                self.caps[i] *= 2
-                setattr(self, names[i], self._grown(getattr(self, names[i]), self.caps[i]))
+        for i, req in enumerate(self.required(cur)):
+            if req > self.caps[i]:
+                cap = self.caps[i]
+                while cap < req:
+                    cap *= 2
+                self.caps[i] = cap
+                setattr(self, names[i], self._grown(getattr(self, names[i]), cap))
         self.cursor[:, _abi.CUR_FULL] = 0
 
     def buffer(self, final_wall: torch.Tensor) -> "ArenaRolloutBuffer":

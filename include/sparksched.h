@@ -278,7 +278,8 @@ typedef struct ssim_decima_sample { /* 64 B, one per decision */
 typedef struct ssim_decima_samples {
   int32_t* cursor;             /* device int32 [num_envs][8]: samples, node rows, edge rows, DAG rows used (the caller
                                   zeroes it before a collection); [4] = 1 when the env stopped because a region was full
-                                  (grow the arena, clear the flag, launch again: the env continues where it stopped) */
+                                  (grow the arena, clear the flag, launch again: the env continues where it stopped);
+                                  [5..7] = the node, edge and DAG rows the observation that did not fit needs */
   ssim_decima_sample* rec;     /* [num_envs][cap_samples] */
   float* nodes;                /* [num_envs][cap_nodes][6]: the 5 Decima node features, then the schedulable flag */
   int32_t* edges;              /* [num_envs][cap_edges][4]: parent, child (node rows of the observation), edge-mask word, 0 */

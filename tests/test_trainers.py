@@ -500,9 +500,13 @@ def test_arena_buffer_matches_per_step_batches(dataset):
             need = [int(arena.cursor[e, 0]) + 1, int(arena.cursor[e, 1]) + int(v["counts"][e][_abi.OC_NUM_NODES]),
                     int(arena.cursor[e, 2]) + int(v["counts"][e][_abi.OC_NUM_EDGES]),
                     int(arena.cursor[e, 3]) + int(v["counts"][e][_abi.OC_NUM_JOBS])]
-            while any(n > c for n, c in zip(need, arena.caps)):  # the kernel's full flag, then the host's growth
+            if any(n > c for n, c in zip(need, arena.caps)):  # the kernel's full flag and needs, the host's growth
                 arena.cursor[e, _abi.CUR_FULL] = 1
+                arena.cursor[e, _abi.CUR_NEED_NODES] = int(v["counts"][e][_abi.OC_NUM_NODES])
+                arena.cursor[e, _abi.CUR_NEED_EDGES] = int(v["counts"][e][_abi.OC_NUM_EDGES])
+                arena.cursor[e, _abi.CUR_NEED_DAGS] = int(v["counts"][e][_abi.OC_NUM_JOBS])
                 arena.grow(arena.cursor.numpy())
+                assert all(n <= c for n, c in zip(need, arena.caps)), (need, arena.caps)  # one growth fits it
             _fill_arena_like_kernel(arena, e, v, f)
         eng.rollout(_abi.SSIM_POLICY_RANDOM, 5, 1)
     assert arena.caps[0] >= 12 and arena.caps[1] > 64  # grew
@@ -651,3 +655,20 @@ def test_decima_budget_not_spent_on_truncated_envs(gpu_device, dataset):
     assert last <= 6, (last, [c.tolist() for c in counts])
     # from then on every launch's whole budget went to the live envs
     assert added[last + 1:] == [budget] * (len(added) - last - 1), added
+
+
+def test_arena_grows_the_region_that_overflowed():
+    """DecimaSampleArena.grow sizes each region from what the stopped observation needs (the kernel records its
+    node / edge / DAG rows in cursor[5..7]): a node region 40k of 64k used that a 30k-node observation overflows
+    grows to fit in one step, and an edge region that is 7/8 used but fits is left alone."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.trainers.rollouts import DecimaSampleArena
+
+    arena = DecimaSampleArena(2, "cpu", cap_samples=16, cap_nodes=1 << 16, cap_edges=1 << 10, cap_dags=64)
+    cur = arena.cursor.numpy()
+    cur[0, [_abi.CUR_SAMPLES, _abi.CUR_NODES, _abi.CUR_EDGES, _abi.CUR_DAGS]] = [3, 40000, 896, 10]
+    cur[0, [_abi.CUR_FULL, _abi.CUR_NEED_NODES, _abi.CUR_NEED_EDGES, _abi.CUR_NEED_DAGS]] = [1, 30000, 20, 4]
+    cur[1, [_abi.CUR_SAMPLES, _abi.CUR_NODES]] = [15, 100]  # not full: ignored
+    arena.grow(cur)
+    assert arena.caps == [16, 1 << 17, 1 << 10, 64], arena.caps
+    assert arena.nodes.shape[1] == 1 << 17 and not (arena.cursor[:, _abi.CUR_FULL] != 0).any()
