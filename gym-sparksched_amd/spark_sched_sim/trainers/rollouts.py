@@ -262,7 +262,7 @@ class DecimaSampleArena:
                     cap *= 2
                 self.caps[i] = cap
                 setattr(self, names[i], self._grown(getattr(self, names[i]), cap))
-        self.cursor[:, _abi.CUR_FULL] = 0
+        self.cursor[:, _abi.CUR_FULL:] = 0  # the flags and the recorded needs
 
     def buffer(self, final_wall: torch.Tensor) -> "ArenaRolloutBuffer":
         return ArenaRolloutBuffer(self, final_wall)
