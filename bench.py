@@ -141,7 +141,7 @@ def _cpu_worker(args):
     import numpy as np
 
     from oracle.policies import FairPolicy, RandomPolicy
-    from oracle.restatement import SparkSchedOracle
+    from oracle.restatement import InvariantError, SparkSchedOracle
     from spark_sched_sim.data_samplers.synthetic_tpch import generate
     from spark_sched_sim.wrappers import StochasticTimeLimit
 
@@ -183,24 +183,35 @@ def _cpu_worker(args):
 
         def act(obs):
             return pol.schedule(obs)[0]
-    ep = 0
+    def step(obs):
+        # The reference asserts "[step]" (spark_sched_sim.py:214-217) when a round's simulation drains the event
+        # queue without a decision to make before every job completes; the oracle raises InvariantError there. A
+        # worker process would die on it, so the harness ends that episode instead and counts it (aborted).
+        try:
+            o, _, term, trunc, _ = env.step(act(obs))
+            return o, term or trunc, False
+        except InvariantError:
+            return None, True, True
+
+    ep, aborted = 0, 0
     obs, _ = env.reset(seed=seed)
     t_w = time.perf_counter()
     while time.perf_counter() - t_w < warm_s:  # warm-up: one episode (bounded)
-        obs, _, term, trunc, _ = env.step(act(obs))
-        if term or trunc:
+        obs, done, _ = step(obs)
+        if done:
             break
     ep += 1
     obs, _ = env.reset(seed=seed + 1000 * ep)
     decisions, episodes, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        obs, _, term, trunc, _ = env.step(act(obs))
+        obs, done, bad = step(obs)
         decisions += 1
-        if term or trunc:
+        aborted += bad
+        if done:
             ep += 1
             episodes += 1
             obs, _ = env.reset(seed=seed + 1000 * ep)
-    return decisions, time.perf_counter() - t0, episodes
+    return decisions, time.perf_counter() - t0, episodes, aborted
 
 
 def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0, ds_seed: int = 0) -> dict:
@@ -218,7 +229,8 @@ def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0,
     return {"value": value, "unit": "decisions/s", "cores": procs, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus": host, "usable_cpus": usable_cpus(),
             "per_core": value / procs, "projected_host": value / procs * host,
-            "episodes_finished": int(sum(r[2] for r in res)), "seconds": wall,
+            "episodes_finished": int(sum(r[2] for r in res)), "episodes_aborted": int(sum(r[3] for r in res)),
+            "seconds": wall,
             "sample": f"{procs} spawn processes (one per usable CPU of this job) x {seconds:.0f} s after a "
                       f"1-episode warm-up, {workload} workload (J={wl['cfg']['job_arrival_cap']}, "
                       f"N={wl['cfg']['num_executors']}, {wl['policy']} policy), one env per process: the CPU "

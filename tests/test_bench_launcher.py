@@ -59,6 +59,6 @@ def test_launcher_one_rank_reports_ranks_seen():
 def test_cpu_baseline_worker(workload):
     import bench
 
-    dec, wall, _ = bench._cpu_worker((workload, 3, 1.0, 0.5, 0))
+    dec, wall, _, _ = bench._cpu_worker((workload, 3, 1.0, 0.5, 0))
     assert dec > 0 and wall >= 1.0
     assert bench.usable_cpus() >= 1 and isinstance(bench.cpu_model(), str)
