@@ -19,6 +19,9 @@ def main():
     from spark_sched_sim.schedulers import decima as D
     from spark_sched_sim.trainers import DECIMA_TPCH, PPO
 
+    if os.environ.get("LEARNER_BLAS"):  # A/B of the BLAS backend (cublas = hipBLAS/rocBLAS, cublaslt = hipBLASLt)
+        torch.backends.cuda.preferred_blas_library(os.environ["LEARNER_BLAS"])
+        print("blas", torch.backends.cuda.preferred_blas_library(), flush=True)
     cfg = {k: dict(v) for k, v in DECIMA_TPCH.items()}
     dev = torch.device("cuda:0")
     ppo = PPO(cfg["agent"], cfg["env"], cfg["trainer"], dataset=generate(0), device=dev)
