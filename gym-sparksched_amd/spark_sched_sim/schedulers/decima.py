@@ -37,6 +37,8 @@ import torch.nn as nn
 
 from .. import _abi
 
+from .linear import HipLinear  # noqa: E402
+
 NUM_NODE_FEATURES = 5  # env_wrapper.py:9
 NUM_DAG_FEATURES = 3   # scheduler.py:34
 DECIMA_PARAMS = 20802  # parameters of the decima_tpch.yaml architecture (the fused kernel's; csrc/decima_policy.h)
@@ -50,7 +52,7 @@ def make_mlp(input_dim: int, hid_dims: list[int], output_dim: int, act_cls: str,
     prev = input_dim
     dims = list(hid_dims) + [output_dim]
     for i, d in enumerate(dims):
-        mlp.append(nn.Linear(prev, d))
+        mlp.append(HipLinear(prev, d))  # nn.Linear; its device passes on csrc/k_linear.hip
         if i == len(dims) - 1:
             break
         mlp.append(act(**(act_kwargs or {})))

@@ -315,6 +315,20 @@ const char* ssim_last_error(void);
 int ssim_debug_set_trace(ssim_handle* h, const int32_t* ops, int32_t n_ops, int32_t width, int32_t* orders,
                          void* stream);
 
+/* The PPO learner's small dense layers (widths <= 64: the Decima MLPs) on the device, replacing the nn.Linear GEMMs
+ * of trainers/ppo.py's evaluate_actions passes (reference: schedulers/decima/utils.py:51-70 make_mlp, trained by
+ * trainers/ppo.py:105-138). Row-major f32 device arrays; returns 0, or -1 for widths outside 1..64.
+ * ssim_linear_fwd: y[r][j] = b[j] + sum_i x[r][i] * w(i, j), w(i, j) = w[j * in_dim + i] if transpose_w (nn.Linear's
+ * [out][in] weight: the forward) else w[i * out_dim + j] (the input gradient, dX = dY W); b may be NULL.
+ * ssim_linear_wgrad: gw[j][i] = sum_r gy[r][j] * x[r][i], gb[j] = sum_r gy[r][j] (gb may be NULL), through
+ * `partial` (parts x out_dim x (in_dim + 1) floats; parts = ssim_linear_wgrad_parts(rows)), summed in chunk order:
+ * deterministic. */
+int ssim_linear_fwd(const float* x, const float* w, const float* b, float* y, int64_t rows, int32_t in_dim,
+                    int32_t out_dim, int32_t transpose_w, void* stream);
+int32_t ssim_linear_wgrad_parts(int64_t rows);
+int ssim_linear_wgrad(const float* gy, const float* x, float* gw, float* gb, int64_t rows, int32_t in_dim,
+                      int32_t out_dim, float* partial, int32_t parts, void* stream);
+
 /* Identity of this build: a hash of the library's kernel sources and compile definitions (__graft_entry__.build_lib).
  * bench.py quotes PMC traffic only from a PMC summary (profiles/) made with the same build. */
 const char* ssim_build_id(void);
