@@ -29,12 +29,12 @@ def make(gpu_device):
     return _make
 
 
-@pytest.mark.parametrize("K,warmup,stride", [(20, 5, 1), (300, 50, 16)])
+@pytest.mark.parametrize("K,warmup,stride", [(20, 5, 1), (300, 50, 4)])
 def test_bench_tpch_timed_launch_replay(make, dataset, K, warmup, stride):
     """configs[1] as the driver times it (`bench.py --steps 20 --warmup 5`) and as bench.py's default (300 / 50):
     1024 envs on the LDS-resident bench kernel, pre-roll in [0, 1000) with auto-reset, the PREEMPT | AUTORESET
     budget launches, a closing launch. The driver's sequence replays EVERY env on the oracle (obs, wall time, job
-    times, episodes, decisions; fanned out over the box's CPUs), the 300-step one every 16th."""
+    times, episodes, decisions; fanned out over the box's CPUs), the 300-step one every 4th."""
     r = cases.case_bench_rollout_sequence(make, dataset, TPCH, B=1024, preroll=1000, warmup=warmup, K=K, stride=stride,
                                           expect_resident=True)
     assert r["envs_replayed"] >= 1024 // stride
@@ -45,17 +45,17 @@ def test_bench_tpch_timed_launch_replay(make, dataset, K, warmup, stride):
 def test_bench_tpch_large_batch_hbm_replay(make, dataset):
     """configs[1]'s env at 4096 envs per GPU (`bench.py --envs 4096`): a batch past 1.5x what the LDS-resident kernel
     holds at once runs on the HBM-resident (10 executors, 50 jobs)-specialised kernels (layout.h lds_concurrent_envs,
-    k_hbm_n10.hip). bench.py's 300-step sequence; every 64th env replayed on the oracle."""
-    r = cases.case_bench_rollout_sequence(make, dataset, TPCH, B=4096, preroll=1000, warmup=50, K=300, stride=64,
+    k_hbm_n10.hip). bench.py's 300-step sequence; every 4th env replayed on the oracle."""
+    r = cases.case_bench_rollout_sequence(make, dataset, TPCH, B=4096, preroll=1000, warmup=50, K=300, stride=4,
                                           expect_resident=False)
-    assert r["envs_replayed"] >= 4096 // 64
+    assert r["envs_replayed"] >= 4096 // 4
     assert r["crossed_replayed"] >= 1
 
 
 def test_bench_tpch_timed_launch_replay_traced(make, dataset):
     """The same sequence with event tracing on (trace records are written by a uniform branch the bench skips): the
     replayed envs' current-episode event traces (event order, executors, stage / job completions) bit for bit."""
-    r = cases.case_bench_rollout_sequence(make, dataset, TPCH, B=1024, preroll=1000, warmup=5, K=20, stride=64,
+    r = cases.case_bench_rollout_sequence(make, dataset, TPCH, B=1024, preroll=1000, warmup=5, K=20, stride=16,
                                           trace_cap=12000, expect_resident=True)
     assert r["pending_at_timed_end"] > 0
 
@@ -63,27 +63,30 @@ def test_bench_tpch_timed_launch_replay_traced(make, dataset):
 def test_bench_large_shard_deep_replay(make, dataset):
     """configs[3] shard as bench.py --workload large runs it: 4096 envs, J=200 / N=100, StochasticTimeLimit mean 2e7,
     the HBM-resident 4-wave kernel, pre-roll in [0, 3000) (hundreds of active stages), then the warm-up and timed
-    budget launches; every 512th env replayed."""
-    r = cases.case_bench_rollout_sequence(make, dataset, LARGE, B=4096, preroll=3000, warmup=5, K=20, stride=512,
+    budget launches; every 8th env replayed (512 envs, fanned out over the box's CPUs)."""
+    r = cases.case_bench_rollout_sequence(make, dataset, LARGE, B=4096, preroll=3000, warmup=5, K=20, stride=8,
                                           mean_limit=2.0e7, expect_resident=False)
-    assert r["decisions_replayed"] > 4 * 1500
+    assert r["envs_replayed"] >= 4096 // 8
+    assert r["decisions_replayed"] > 256 * 1500
 
 
 def test_bench_decima_env_deep_replay_hbm_rollout(make, dataset):
     """The configs[2] env shape on the HBM-resident rollout kernel 1500+ decisions deep (4096 envs, J=200 / N=50,
-    time limits): the pre-roll of bench.py --workload decima, then budget launches; every 512th env replayed."""
-    cases.case_bench_rollout_sequence(make, dataset, DECIMA, B=4096, preroll=3000, warmup=5, K=20, stride=512,
-                                      mean_limit=2.0e7, expect_resident=False)
+    time limits): the pre-roll of bench.py --workload decima, then budget launches; every 8th env replayed."""
+    r = cases.case_bench_rollout_sequence(make, dataset, DECIMA, B=4096, preroll=3000, warmup=5, K=20, stride=8,
+                                          mean_limit=2.0e7, expect_resident=False)
+    assert r["envs_replayed"] >= 4096 // 8
 
 
 def test_bench_decima_persistent_rollout_replay(make, dataset):
     """configs[2] as bench.py --workload decima now times it: 4096 envs (J=200 / N=50, time limits), the pre-roll,
     then the warm-up and timed persistent Decima rollouts (ssim_decima_rollout: features, fused GNN policy and step
-    per env in one launch, a shared budget, PREEMPT | AUTORESET) and a closing launch; every 512th env's actions
+    per env in one launch, a shared budget, PREEMPT | AUTORESET) and a closing launch; every 8th env's actions
     replayed on the oracle across its episode boundaries."""
-    r = cases.case_bench_rollout_sequence(make, dataset, DECIMA, B=4096, preroll=1500, warmup=5, K=20, stride=512,
+    r = cases.case_bench_rollout_sequence(make, dataset, DECIMA, B=4096, preroll=1500, warmup=5, K=20, stride=8,
                                           mean_limit=2.0e7, expect_resident=False, policy="decima")
-    assert r["decisions_replayed"] > 8 * 700
+    assert r["envs_replayed"] >= 4096 // 8
+    assert r["decisions_replayed"] > 512 * 700
 
 
 def test_decima_persistent_rollout_small_batch_replay(make, dataset):
@@ -125,7 +128,7 @@ def test_forced_hbm_bench_sequence(make, dataset):
 def test_bench_decima_timed_steps_replay(gpu_device, dataset):
     """configs[2] as bench.py --workload decima times it: 4096 envs (J=200, N=50, StochasticTimeLimit mean 2e7),
     pre-roll in [0, 1500) with auto-reset, then per decision the fused Decima policy launch, the HBM-resident k_step
-    launch and the device reset of finished episodes (ssim_reset_sampled). Every 512th env's actions (pre-roll and
+    launch and the device reset of finished episodes (ssim_reset_sampled). Every 16th env's actions (pre-roll and
     policy steps) replayed on the oracle across its episode boundaries."""
     import torch
 
@@ -134,7 +137,7 @@ def test_bench_decima_timed_steps_replay(gpu_device, dataset):
     from spark_sched_sim.schedulers.decima import DecimaScheduler
 
     SENT = -99
-    B, W, K, stride = 4096, 5, 20, 512
+    B, W, K, stride = 4096, 5, 20, 16
     dev = torch.device(gpu_device)
     eng = DeviceEngine(DECIMA, B, dataset, device=gpu_device)
     assert int(eng.layout.lds_resident) == 0
@@ -170,6 +173,7 @@ def test_bench_decima_timed_steps_replay(gpu_device, dataset):
         actions[i].extend(st[:, i].tolist())
     v = eng.host_views()
     ta, tc, _ = eng.job_times_np()
-    for i in range(0, B, stride):
-        o, ob, ep, dec, last = cases.replay_with_autoreset(DECIMA, dataset, seeds[i], lim[i], actions[i])
+    sample = list(range(0, B, stride))
+    res = cases.replay_many(DECIMA, dataset, [(seeds[i], lim[i], actions[i]) for i in sample])
+    for i, (o, ob, ep, dec, last) in zip(sample, res):
         cases.check_replayed_env(eng, v, ta, tc, i, o, ob, ep, dec, last, "decima-bench")
