@@ -92,13 +92,13 @@ def case_rollout_replay(make, dataset, env_cfg, kind, B=64, K=400, stride=4, bud
         assert dec.sum() <= B * budget and (dec.sum() == B * budget or not live.any())
         assert dec.max() > dec.min()  # the budget went unevenly (cheap envs took more)
     ta, tc, _ = eng.job_times_np()
-    for i in range(0, B, stride):
-        o = SparkSchedOracle(env_cfg, dataset)
-        o.trace = []
-        ob, _ = o.reset(seed=seeds[i])
+    sample = list(range(0, B, stride))
+    # many envs: the replays fanned out over the CPUs (cases.replay_many), otherwise in this process
+    items = [(seeds[i], None, log[: int(v["counts"][i][_abi.OC_DECISIONS]), i].tolist()) for i in sample]
+    done = replay_many(env_cfg, dataset, items, trace=True, autoreset=False) if len(sample) >= 16 else [
+        replay_with_autoreset(env_cfg, dataset, s_, None, a_, trace=True, autoreset=False) for s_, _, a_ in items]
+    for i, (o, ob, _, _, _) in zip(sample, done):
         c = v["counts"][i]
-        for k in range(int(c[_abi.OC_DECISIONS])):
-            ob, rew, term, _, info = o.step({"stage_idx": int(log[k, i, 0]), "num_exec": int(log[k, i, 1])})
         assert int(c[_abi.OC_ERR]) == 0
         assert bool(c[_abi.OC_TERMINATED]) == o.terminated
         assert float(v["wall_time"][i]) == float(o.wall_time)
@@ -624,11 +624,11 @@ def bench_time_limits(mean_limit, seeds):
     return np.array([smp.sample(i, int(seeds[i])) for i in range(len(seeds))], dtype=np.float64)
 
 
-def replay_with_autoreset(cfg, dataset, seed, limit, actions, trace=False):
+def replay_with_autoreset(cfg, dataset, seed, limit, actions, trace=False, autoreset=True):
     """The oracle driven through `actions` from reset(seed), restarting like the device's auto-reset: after a step
-    that terminates the episode or reaches its time limit, reset(seed=None) with the same limit. Returns the oracle,
-    its last observation, the episode count, the decisions of the current episode and the last step's reward (None
-    if the last step ended an episode)."""
+    that terminates the episode or reaches its time limit, reset(seed=None) with the same limit (autoreset=False:
+    never, the launches without SSIM_ROLLOUT_AUTORESET). Returns the oracle, its last observation, the episode count,
+    the decisions of the current episode and the last step's reward (None if the last step ended an episode)."""
     limit = float("inf") if limit is None else float(limit)
     o = SparkSchedOracle(cfg, dataset)
     if trace:
@@ -638,7 +638,7 @@ def replay_with_autoreset(cfg, dataset, seed, limit, actions, trace=False):
     for a in actions:
         ob, rew, term, _, info = o.step({"stage_idx": int(a[0]), "num_exec": int(a[1])})
         dec, last = dec + 1, rew
-        if term or info["wall_time"] >= limit:
+        if autoreset and (term or info["wall_time"] >= limit):
             if trace:
                 o.trace = []
             ob, _ = o.reset(seed=None, options={"time_limit": limit})
@@ -655,6 +655,7 @@ class _Replayed:
         self.wall_time = o.wall_time
         self.jobs = {jid: SimpleNamespace(t_arrival=j.t_arrival, t_completed=j.t_completed) for jid, j in o.jobs.items()}
         self.trace = getattr(o, "trace", None)
+        self.terminated = o.terminated
 
 
 _POOL_DATASET = None
@@ -666,12 +667,13 @@ def _pool_init(dataset):
 
 
 def _replay_one(args):
-    cfg, seed, limit, actions, trace = args
-    o, ob, ep, dec, last = replay_with_autoreset(cfg, _POOL_DATASET, seed, limit, actions, trace=trace)
+    cfg, seed, limit, actions, trace, autoreset = args
+    o, ob, ep, dec, last = replay_with_autoreset(cfg, _POOL_DATASET, seed, limit, actions, trace=trace,
+                                                 autoreset=autoreset)
     return _Replayed(o), ob, ep, dec, last
 
 
-def replay_many(cfg, dataset, items, trace=False):
+def replay_many(cfg, dataset, items, trace=False, autoreset=True):
     """replay_with_autoreset for many envs, fanned out over the CPUs this job may use (spawn processes: the
     parent holds a GPU context). items: (seed, limit, actions) per env. Returns (oracle view, obs, episodes,
     decisions, last reward) per env, in order."""
@@ -679,7 +681,7 @@ def replay_many(cfg, dataset, items, trace=False):
 
     import bench
 
-    jobs = [(cfg, s, lim, a, trace) for s, lim, a in items]
+    jobs = [(cfg, s, lim, a, trace, autoreset) for s, lim, a in items]
     procs = min(bench.usable_cpus(), 16, len(jobs))
     if procs <= 1:
         return [_replay_one_local(dataset, j) for j in jobs]
@@ -688,8 +690,8 @@ def replay_many(cfg, dataset, items, trace=False):
 
 
 def _replay_one_local(dataset, job):
-    cfg, seed, limit, actions, trace = job
-    o, ob, ep, dec, last = replay_with_autoreset(cfg, dataset, seed, limit, actions, trace=trace)
+    cfg, seed, limit, actions, trace, autoreset = job
+    o, ob, ep, dec, last = replay_with_autoreset(cfg, dataset, seed, limit, actions, trace=trace, autoreset=autoreset)
     return o, ob, ep, dec, last
 
 

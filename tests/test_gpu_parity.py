@@ -54,7 +54,7 @@ def test_rollout_preempt_replay(make, dataset, env_cfg, autoreset):
 
 
 def test_rollout_replay_full_episodes(make, dataset, env_cfg):
-    cases.case_rollout_replay(make, dataset, env_cfg, _abi.SSIM_POLICY_RANDOM, B=256, K=2500, stride=32)
+    cases.case_rollout_replay(make, dataset, env_cfg, _abi.SSIM_POLICY_RANDOM, B=256, K=2500, stride=4)
 
 
 def test_invalid_actions(make, dataset, env_cfg):
@@ -102,16 +102,16 @@ def test_render_history_device(gpu_device, dataset, env_cfg):
 def test_full_size_bench_shape_budget_replay(make, dataset, env_cfg):
     """BASELINE configs[1] at full size (1024 envs, 50 jobs / 10 executors, the bench's kernel instantiation
     and shared-budget launch of 300 decisions per env): every env error-free, the budget spent exactly, and
-    every 64th env replayed on the oracle bit-exactly (trace, job times, final observation)."""
-    cases.case_rollout_replay(make, dataset, env_cfg, _abi.SSIM_POLICY_RANDOM, B=1024, K=2400, stride=64,
+    every 8th env replayed on the oracle bit-exactly (trace, job times, final observation)."""
+    cases.case_rollout_replay(make, dataset, env_cfg, _abi.SSIM_POLICY_RANDOM, B=1024, K=2400, stride=8,
                               budget=300)
 
 
 def test_full_size_large_shard_replay(make, dataset, env_cfg):
     """BASELINE configs[3] per-GPU shard at full size (4096 envs, 200 jobs / 100 executors, the HBM-resident
-    kernel compiled for 4 waves/SIMD): 40 fused decisions per env, every 512th env replayed on the oracle."""
+    kernel compiled for 4 waves/SIMD): 40 fused decisions per env, every 16th env replayed on the oracle."""
     cfg = dict(env_cfg, num_executors=100, job_arrival_cap=200)
-    cases.case_rollout_replay(make, dataset, cfg, _abi.SSIM_POLICY_RANDOM, B=4096, K=40, stride=512)
+    cases.case_rollout_replay(make, dataset, cfg, _abi.SSIM_POLICY_RANDOM, B=4096, K=40, stride=16)
 
 
 @pytest.mark.parametrize("name", __import__("test_golden").NAMES)
