@@ -14,10 +14,17 @@ from torch import nn
 _MAX = 64
 
 
-def _lib():
-    from .. import native
+_FN = None  # (fwd, wgrad_parts, wgrad, check): bound once (each learner pass makes ~6k calls)
 
-    return native
+
+def _fns():
+    global _FN
+    if _FN is None:
+        from .. import native
+
+        L = native.lib()
+        _FN = (L.ssim_linear_fwd, L.ssim_linear_wgrad_parts, L.ssim_linear_wgrad, native.check)
+    return _FN
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -27,21 +34,21 @@ def _stream(t: torch.Tensor) -> int:
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None):
-        nat = _lib()
+        fwd, _, _, check = _fns()
         x = x.contiguous()
         w = w.contiguous()
         rows, k = x.shape
         n = w.shape[0]
         y = torch.empty((rows, n), dtype=torch.float32, device=x.device)
-        nat.check(nat.lib().ssim_linear_fwd(x.data_ptr(), w.data_ptr(), None if b is None else b.data_ptr(),
-                                            y.data_ptr(), rows, k, n, 1, _stream(x)), "ssim_linear_fwd")
+        check(fwd(x.data_ptr(), w.data_ptr(), None if b is None else b.data_ptr(), y.data_ptr(), rows, k, n, 1,
+                  _stream(x)), "ssim_linear_fwd")
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         return y
 
     @staticmethod
     def backward(ctx, gy: torch.Tensor):
-        nat = _lib()
+        fwd, wgrad_parts, wgrad, check = _fns()
         x, w = ctx.saved_tensors
         gy = gy.contiguous()
         rows, k = x.shape
@@ -50,16 +57,15 @@ class _LinearFn(torch.autograd.Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty((rows, k), dtype=torch.float32, device=gy.device)
-            nat.check(nat.lib().ssim_linear_fwd(gy.data_ptr(), w.data_ptr(), None, gx.data_ptr(), rows, n, k, 0, s),
-                      "ssim_linear_fwd (input gradient)")
+            check(fwd(gy.data_ptr(), w.data_ptr(), None, gx.data_ptr(), rows, n, k, 0, s),
+                  "ssim_linear_fwd (input gradient)")
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            parts = int(nat.lib().ssim_linear_wgrad_parts(rows))
+            parts = int(wgrad_parts(rows))
             part = torch.empty((parts, n * (k + 1)), dtype=torch.float32, device=gy.device)
             gw = torch.empty((n, k), dtype=torch.float32, device=gy.device)
             gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
-            nat.check(nat.lib().ssim_linear_wgrad(gy.data_ptr(), x.data_ptr(), gw.data_ptr(),
-                                                  None if gb is None else gb.data_ptr(), rows, k, n, part.data_ptr(),
-                                                  parts, s), "ssim_linear_wgrad")
+            check(wgrad(gy.data_ptr(), x.data_ptr(), gw.data_ptr(), None if gb is None else gb.data_ptr(), rows, k,
+                        n, part.data_ptr(), parts, s), "ssim_linear_wgrad")
         return gx, gw, gb
 
 
