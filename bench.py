@@ -205,7 +205,7 @@ def _cpu_worker(args):
     decisions, episodes, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         obs, done, bad = step(obs)
-        decisions += 1
+        decisions += not bad  # a step the [step] assertion aborted never completed: not a decision
         aborted += bad
         if done:
             ep += 1

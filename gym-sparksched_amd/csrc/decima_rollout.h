@@ -49,6 +49,7 @@ struct DecimaRolloutArgs {
   float num_tasks_scale, work_scale;
   uint64_t seed, counter;
   int32_t autoreset;
+  int32_t test_reject;      // SSIM_ROLLOUT_TEST_REJECT (test hook): the launch's first decision asks for N + 1 executors
   ssim_decima_samples smp;  // smp.rec == nullptr: no sample arena
 };
 
@@ -86,7 +87,7 @@ struct DecimaPolicy {
     return true;
   }
   template <class S>
-  __device__ __forceinline__ bool act(S& s, int /*k*/, StepIn* out) const {
+  __device__ __forceinline__ bool act(S& s, int k, StepIn* out) const {
     using W = WaveHip;
     const ssim_layout& L = P->L;
     const int eid = s.eid;
@@ -129,6 +130,7 @@ struct DecimaPolicy {
                             wk + a.wl.plan, none, &act, pprof);
     out->stage_idx = act.stage_idx;
     out->num_exec = act.num_exec;
+    if (a.test_reject && k == 0) out->num_exec = L.num_executors + 1;  // (test hook: an action the env refuses)
 #ifdef SSIM_PROFILE
     s.prof_add(kPhDecPolicy, W::clock() - tp);
     tp = W::clock();
@@ -202,6 +204,27 @@ struct DecimaPolicy {
     if (W::lane() == 0 && cs > 0) sm.rec[(int64_t)eid * sm.cap_samples + cs - 1].reward = r;
     W::sync();
   }
+  // The env refused the action act() recorded (it is frozen with SSIM_ERR_INVARIANT, the collector raises): the
+  // sample and its observation rows come off the arena, so no sample ever holds an action the env did not take.
+  template <class S>
+  __device__ __forceinline__ void rejected(S& s) const {
+    using W = WaveHip;
+    const ssim_decima_samples& sm = a.smp;
+    if (sm.rec == nullptr) return;
+    W::sync();
+    if (W::lane() == 0) {
+      int32_t* cur = sm.cursor + (int64_t)s.eid * 8;
+      const int cs = cur[0];
+      if (cs > 0) {
+        const ssim_decima_sample& r = sm.rec[(int64_t)s.eid * sm.cap_samples + cs - 1];
+        cur[1] -= r.num_nodes;
+        cur[2] -= r.num_edges;
+        cur[3] -= r.num_dags;
+        cur[0] = cs - 1;
+      }
+    }
+    W::sync();
+  }
 };
 
 #ifndef SSIM_DECIMA_ROLLOUT_WAVES
@@ -214,6 +237,7 @@ __device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P
                                                     const double* __restrict__ limits, uint8_t* reset,
                                                     int32_t* action_log, int64_t budget, uint64_t* prof_out) {
   a.autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
+  a.test_reject = (flags & SSIM_ROLLOUT_TEST_REJECT) != 0;
   const DecimaPolicy pol{P, obs, a};
   rollout_body<kRes, kN, kJ, 0, DecimaPolicy, kWS, kWJ>(P, state, obs, pol, num_steps, flags, limits, reset, action_log,
                                                        prof_out, budget, nullptr);
@@ -240,6 +264,8 @@ using DecimaRolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, DecimaRollou
                                  uint8_t*, int32_t*, int64_t, uint64_t*);
 struct DecimaRolloutSet {
   DecimaRolloutFn rollout, rollout_warmup;
+  SetTraceFn set_trace;  // the set KAT through this unit's engine instantiation (kernels.h k_set_trace)
+  const char* name;      // the translation unit (ssim_debug_kernel_name)
   int win_jobs = 0, win_stages = 0;  // windowed engine: ring sizes
 };
 DecimaRolloutSet decima_rollout_hbm();    // k_dr_hbm.hip

@@ -51,6 +51,18 @@
 
 namespace ssim {
 
+// Test-only wave types (the set KAT's known-bad variant, tests/test_gpu_sets.py) declare kKatBadPage = true; the paged
+// set code then reproduces the effect of the ROCm 7.2 miscompile it works around (Sim::paged_set), so the KAT can be
+// shown to catch it. Every shipped wave type leaves it undeclared (false).
+template <class W, class = void>
+struct KatBadPage {
+  static constexpr bool value = false;
+};
+template <class W>
+struct KatBadPage<W, decltype((void)W::kKatBadPage)> {
+  static constexpr bool value = W::kKatBadPage;
+};
+
 // Dataset pointers are loaded from the Params block, so the compiler sees generic pointers and would emit
 // FLAT loads; the cast to the global address space turns them into global_load (test host build: no-op).
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1289,7 +1301,14 @@ struct Sim {
                                                     int* dummy) {
     uint32_t i = key & mask, perturb = key;
     int fd = -1;
-    for (;;) {
+    for (int it = 0;; ++it) {
+      if constexpr (KatBadPage<W>::value) {  // the known-bad KAT variant may corrupt a table past any EMPTY slot:
+        if (it > 4096) {                     // end its walk instead of spinning
+          *empty = -1;
+          *dummy = -1;
+          return -1;
+        }
+      }
       const uint32_t wn = (i + 9u <= mask) ? 10u : 1u;
       uint32_t E, D, K;
       paged_win(v, i, wn, key, &E, &D, &K);
@@ -1318,7 +1337,9 @@ struct Sim {
   __device__ __forceinline__ static uint64_t page_of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
   // pages 0 and 1 hold b0 / b1 (EMPTY elsewhere): the clean-insert tables whose keys are all below 128
   __device__ __forceinline__ static uint64_t page01(uint32_t b0, uint32_t b1) {
-    return page_of(0xFFFF0000u | (b1 << 8) | b0, 0xFFFFFFFFu);
+    // (the test-only KAT wave type reproduces the miscompiled result in one lane: key 0 in slot 256 of a clean-insert
+    // table; the miscompile put it in every lane's pages 4..7, which leaves no bound on the walks that follow)
+    return page_of(0xFFFF0000u | (b1 << 8) | b0, KatBadPage<W>::value && W::lane() == 0 ? 0xFFFFFF00u : 0xFFFFFFFFu);
   }
   __device__ __forceinline__ static uint64_t paged_set(uint64_t v, int slot, int val) {  // the register copy
     const uint32_t g = (uint32_t)(slot >> 6), sh = 8u * (g & 3u);

@@ -3,4 +3,5 @@
 #define SSIM_EV_PAGES_GENERIC 2
 #include "decima_rollout.h"
 
-DecimaRolloutSet decima_rollout_hbm() { return {k_decima_rollout<false>, k_decima_rollout_warmup<false>}; }
+DecimaRolloutSet decima_rollout_hbm() { return {k_decima_rollout<false>, k_decima_rollout_warmup<false>, k_set_trace<WaveHip, false, 0, 0, 0, kTagDrHbm>,
+          "dr_hbm"}; }

@@ -3,5 +3,6 @@
 #include "decima_rollout.h"
 
 DecimaRolloutSet decima_rollout_hbm50() {
-  return {k_decima_rollout<false, 50, 200>, k_decima_rollout_warmup<false, 50, 200>};
+  return {k_decima_rollout<false, 50, 200>, k_decima_rollout_warmup<false, 50, 200>,
+          k_set_trace<WaveHip, false, 50, 200, 0, kTagDrHbm50>, "dr_hbm50"};
 }

@@ -2,4 +2,5 @@
 // of a decima_tpch.yaml PPO iteration, one env per CU with the opt-in 160 KB of LDS).
 #include "decima_rollout.h"
 
-DecimaRolloutSet decima_rollout_lds() { return {k_decima_rollout<true>, k_decima_rollout_warmup<true>}; }
+DecimaRolloutSet decima_rollout_lds() { return {k_decima_rollout<true>, k_decima_rollout_warmup<true>, k_set_trace<WaveHip, true, 0, 0, 0, kTagDrLds>,
+          "dr_lds"}; }

@@ -6,5 +6,5 @@
 DecimaRolloutSet decima_rollout_win50() {
   return {k_decima_rollout<true, 50, 200, kWinStages, kWinJobs>, k_decima_rollout_warmup<true, 50, 200, kWinStages,
                                                                                         kWinJobs>,
-          kWinJobs, kWinStages};
+          k_set_trace<WaveHip, false, 50, 200, 0, kTagDrWin50>, "dr_win50", kWinJobs, kWinStages};
 }

@@ -3,4 +3,4 @@
 #define SSIM_EV_PAGES_GENERIC 2
 #include "kernels.h"
 
-KernelSet kernels_hbm() { return kernel_set<false, 0, 0, 0>(); }
+KernelSet kernels_hbm() { return kernel_set<false, 0, 0, 0, kTagHbm>("hbm"); }

@@ -3,4 +3,4 @@
 // cap is read at run time).
 #include "kernels.h"
 
-KernelSet kernels_hbm_n10() { return kernel_set<false, 10, 50, 0>(); }
+KernelSet kernels_hbm_n10() { return kernel_set<false, 10, 50, 0, kTagHbmN10>("hbm_n10"); }

@@ -3,4 +3,8 @@
 // section offsets and loop bounds into immediates, which takes SGPR pressure (and spills) off the 4-wave kernel.
 #include "kernels.h"
 
-KernelSet kernels_hbm_n100() { return kernel_set<false, 100, 200, 0>(); }
+KernelSet kernels_hbm_n100() { return kernel_set<false, 100, 200, 0, kTagHbmN100>("hbm_n100"); }
+
+// the set KAT's known-bad variant (tests/test_gpu_sets.py): the same instantiation on the test-only wave type that
+// reproduces the ROCm 7.2 page-assembly miscompile (engine.h KatBadPage); it must FAIL the KAT
+SetTraceFn set_trace_kat_bad() { return k_set_trace<WaveHipKatBadPage, false, 100, 200, 0, kTagKatBad>; }

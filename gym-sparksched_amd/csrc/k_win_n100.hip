@@ -4,4 +4,4 @@
 // wave. Steps (k_step) stay HBM-resident.
 #include "kernels.h"
 
-KernelSet kernels_win_n100() { return kernel_set_windowed<100, 200, 0, kWinStages, kWinJobs>(); }
+KernelSet kernels_win_n100() { return kernel_set_windowed<100, 200, 0, kWinStages, kWinJobs, kTagWinN100>("win_n100"); }

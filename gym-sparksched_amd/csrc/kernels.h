@@ -229,24 +229,74 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
                                                             limits, reset, action_log, prof_out, budget, env_steps);
 }
 
+// Test hook (ssim_debug_set_trace_ex, tests/test_gpu_sets.py): a trace of CPython-set operations on one pool (job 0's)
+// of env 0 through the set code of the engine instantiation `Sim<WV, kN, kJ, kS>` with residency kRes — the template
+// instantiation a translation unit's shipped kernels inline, compiled in that unit with its flags (kTag keeps one
+// copy per unit; the linker would otherwise fold identical instantiations of different units into one). The set path
+// is the one the layout selects (one-page lane sets for <= 15 executors, paged tables for 16..127). ops: int32
+// [n_ops][6] = (code, key, busy bitmap words 0..3); code 0 add(key), 1 remove(key), 2 idle order:
+// list(set(e for e in s.copy() if not busy[e])) with the executors' busy flags from the bitmap. orders [n_ops][width]:
+// the set's iteration order after an add / remove, the idle order for code 2; -1 padded. Clobbers env 0.
+template <class WV, bool kRes, int kN, int kJ, int kS, int kTag>
+__global__ __launch_bounds__(64) void k_set_trace(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+                                                  const int32_t* __restrict__ ops, int n_ops, int width,
+                                                  int32_t* orders) {
+  Sim<WV, kN, kJ, kS> s(P, state, g_smem, obs, 0, kRes);
+  if constexpr (kRes) s.load_hot();
+  const int p = s.job_pool(0);
+  ps_init(s.pmeta(p), s.pool(p).tab);
+  int32_t* out = s.template S<int32_t>(s.O.sc_keys_a);
+  for (int k = 0; k < n_ops; ++k) {
+    const int code = WV::uni(ops[6 * k]), key = WV::uni(ops[6 * k + 1]);
+    int n = 0;
+    if (code == 2) {
+      for (int e = WV::lane(); e < s.NE; e += 64)
+        s.exr(e).busy = (int16_t)((ops[6 * k + 2 + (e >> 5)] >> (e & 31)) & 1);
+      WV::sync();
+      n = s.idle_order(p, out);
+    } else {
+      if (code == 0)
+        s.pool_add(p, key);
+      else
+        s.pool_remove(p, key);
+      n = s.table_keys(p, out);
+    }
+    WV::sync();
+    for (int i = WV::lane(); i < width; i += 64) orders[(int64_t)k * width + i] = i < n ? out[i] : -1;
+    WV::sync();
+  }
+}
+// The known-bad wave type of the KAT (engine.h KatBadPage): test-only, never used by a shipped kernel.
+struct WaveHipKatBadPage : WaveHip {
+  static constexpr bool kKatBadPage = true;
+};
+
 using StepFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, const int32_t*);
 using RolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, int, uint64_t, int, int, const double*, uint8_t*,
                           int32_t*, uint64_t*, int64_t, const int32_t*);
+using SetTraceFn = void (*)(const Params*, uint8_t*, uint8_t*, const int32_t*, int, int, int32_t*);
 struct KernelSet {
   StepFn step;
   RolloutFn rollout, rollout_warmup;
+  SetTraceFn set_trace;  // the set KAT through this unit's engine instantiation (k_set_trace)
+  const char* name;      // the translation unit (ssim_debug_kernel_name)
   int win_jobs = 0, win_stages = 0;  // windowed rollouts: ring sizes (0: the rollout's residency is the layout's)
 };
-template <bool kRes, int kN, int kJ, int kS>
-inline KernelSet kernel_set() {
-  return {k_step<kRes, kN, kJ, kS>, k_rollout<kRes, kN, kJ, kS>, k_rollout_warmup<kRes, kN, kJ, kS>};
+template <bool kRes, int kN, int kJ, int kS, int kTag>
+inline KernelSet kernel_set(const char* name) {
+  return {k_step<kRes, kN, kJ, kS>, k_rollout<kRes, kN, kJ, kS>, k_rollout_warmup<kRes, kN, kJ, kS>,
+          k_set_trace<WaveHip, kRes, kN, kJ, kS, kTag>, name};
 }
 // HBM-resident steps, windowed rollouts (rings of kWS stages / kWJ jobs; layout.h window_lds_bytes)
-template <int kN, int kJ, int kS, int kWS, int kWJ>
-inline KernelSet kernel_set_windowed() {
+template <int kN, int kJ, int kS, int kWS, int kWJ, int kTag>
+inline KernelSet kernel_set_windowed(const char* name) {
   return {k_step<false, kN, kJ, kS>, k_rollout<true, kN, kJ, kS, kWS, kWJ>, k_rollout_warmup<true, kN, kJ, kS, kWS, kWJ>,
-          kWJ, kWS};
+          k_set_trace<WaveHip, false, kN, kJ, kS, kTag>, name, kWJ, kWS};
 }
+// Translation-unit tags of k_set_trace (one per k_*.hip)
+enum : int { kTagBench900 = 1, kTagBench, kTagLds, kTagHbm, kTagHbmN100, kTagHbmN10, kTagHbmN50, kTagWinN100, kTagWinN50,
+             kTagDrHbm, kTagDrHbm50, kTagDrLds, kTagDrWin50, kTagKatBad };
+SetTraceFn set_trace_kat_bad();  // k_hbm_n100.hip: the N = 100 / J = 200 instantiation on WaveHipKatBadPage
 // one per translation unit
 KernelSet kernels_bench900();  // k_bench900.hip: LDS-resident, 10 executors / 50 jobs / stage cap 900
 KernelSet kernels_bench();     // k_bench.hip: LDS-resident, 10 executors / 50 jobs, stage cap at run time

@@ -129,10 +129,10 @@ constexpr int64_t kBigLdsMaxEnvs = 256;
 // Measured on configs[1]'s env (profiles/r04/env_sweep_residency.log): LDS 3.55e7 decisions/s at every batch size
 // from 1024 to 8192 envs; HBM-resident (10, 50)-specialised kernels 1.5e7 at 1024, 4.0e7 at 2048, 5.2e7 at 3072,
 // 6.2e7 from 4096. So a batch above 1.5x the LDS-resident concurrency runs HBM-resident.
-constexpr int64_t kChipCus = 256;  // MI355X
-constexpr int64_t lds_concurrent_envs(int64_t need) {
+constexpr int64_t kChipCus = 256;  // a whole MI355X: the default when the device's CU count is not known
+constexpr int64_t lds_concurrent_envs(int64_t need, int64_t chip_cus = kChipCus) {
   const int64_t per_cu = kLdsPerCu / (need > 0 ? need : 1);
-  return kChipCus * (per_cu < 4 ? per_cu : 4);
+  return chip_cus * (per_cu < 4 ? per_cu : 4);
 }
 
 struct TraceRec {  // one popped event
@@ -266,8 +266,10 @@ constexpr int64_t window_lds_bytes(int64_t N, int64_t J, int64_t S, int64_t wj, 
   return win > hbm ? win : hbm;
 }
 
-// Computes the public layout and the private offsets. Returns false on a bad / unsupported config.
-inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets* O) {
+// Computes the public layout and the private offsets. Returns false on a bad / unsupported config. `chip_cus`: the
+// device's compute units (hipDeviceAttributeMultiprocessorCount; a partitioned device or another SKU has fewer), which
+// sets how many envs the LDS-resident kernels hold at once and so the batch size above which they run HBM-resident.
+inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets* O, int64_t chip_cus = kChipCus) {
   if (cfg.num_envs <= 0 || cfg.num_executors <= 0 || cfg.num_executors > 250 || cfg.job_cap <= 0 ||
       cfg.max_stages <= 0 || cfg.max_stages > 128 /* int8 parent countdown */ || cfg.max_edges < 0 ||
       cfg.trace_cap < 0)
@@ -294,7 +296,7 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
   // LDS per wave: [hot copy (if resident) | scratch]
   const int64_t need = O->hot_bytes + O->scratch_bytes;
   O->lds_resident = (!(cfg.flags & SSIM_CFG_FORCE_HBM) &&
-                     ((need <= kLdsBudget && 2 * B <= 3 * lds_concurrent_envs(need)) ||
+                     ((need <= kLdsBudget && 2 * B <= 3 * lds_concurrent_envs(need, chip_cus)) ||
                       (need <= kLdsBudgetBig && B <= kBigLdsMaxEnvs)))
                         ? 1 : 0;
   L->lds_resident = O->lds_resident;

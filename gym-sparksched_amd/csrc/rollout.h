@@ -17,7 +17,8 @@ struct NoBudget : NoStop {
 
 // The action driver of a fused rollout: `act` chooses the next action of the env (false: the env takes no more
 // decisions in this launch, e.g. the Decima collector's episode ended or its sample arena is full), `done` runs after
-// a decision this launch started has completed (its observation written).
+// a decision this launch started has completed (its observation written), `rejected` when the env refused the action
+// act() chose (the env is then frozen with SSIM_ERR_INVARIANT).
 struct HeuristicPolicy {  // fair / FIFO / random (policy.h)
   int kind;
   uint64_t seed;
@@ -34,6 +35,8 @@ struct HeuristicPolicy {  // fair / FIFO / random (policy.h)
   }
   template <class S>
   __device__ __forceinline__ void done(S&) const {}
+  template <class S>
+  __device__ __forceinline__ void rejected(S&) const {}
 };
 
 // The state of one wave's rollout that outlives a switch from the windowed to the HBM-resident engine mid-launch.
@@ -104,6 +107,7 @@ __device__ __forceinline__ int rollout_loop(SimT& s, const Pol& pol, const StopT
       W::sync();
       simulate = s.step_begin(a, &st0);
       if (!simulate && s.rejected) {  // a device policy chose an invalid action: freeze the env (the host sees it)
+        pol.rejected(s);  // (a recording policy drops what it recorded for the refused action)
         s.fail(SSIM_ERR_INVARIANT);
         s.store_header();
         s.write_err_only(0u);

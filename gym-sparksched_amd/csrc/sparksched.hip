@@ -89,40 +89,6 @@ __global__ __launch_bounds__(64) void k_decima_policy(const Params* __restrict__
     atomicAdd(overflow, 1);
 }
 
-// Test hook (tests/test_gpu_sets.py, ssim_debug_set_trace): a trace of CPython-set operations on one pool (job 0's)
-// of env 0, through the engine's own set code on the path the layout selects (one-page lane sets for <= 15
-// executors, paged tables for 16..127, the serial form beyond). ops: int32 [n_ops][6] = (code, key, busy bitmap
-// words 0..3); code 0 add(key), 1 remove(key), 2 idle order: list(set(e for e in s.copy() if not busy[e])) with the
-// executors' busy flags set from the bitmap. orders [n_ops][width]: the set's iteration order after an add / remove,
-// the idle order for code 2; -1 padded.
-__global__ __launch_bounds__(64) void k_debug_set_trace(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
-                                                        const int32_t* __restrict__ ops, int n_ops, int width,
-                                                        int32_t* orders) {
-  Sim<WaveHip> s(P, state, g_smem, obs, 0, false);
-  const int p = s.job_pool(0);
-  ps_init(s.pmeta(p), s.pool(p).tab);
-  int32_t* out = s.template S<int32_t>(s.O.sc_keys_a);
-  for (int k = 0; k < n_ops; ++k) {
-    const int code = WaveHip::uni(ops[6 * k]), key = WaveHip::uni(ops[6 * k + 1]);
-    int n = 0;
-    if (code == 2) {
-      for (int e = WaveHip::lane(); e < s.NE; e += 64)
-        s.exr(e).busy = (int16_t)((ops[6 * k + 2 + (e >> 5)] >> (e & 31)) & 1);
-      WaveHip::sync();
-      n = s.idle_order(p, out);
-    } else {
-      if (code == 0)
-        s.pool_add(p, key);
-      else
-        s.pool_remove(p, key);
-      n = s.table_keys(p, out);
-    }
-    WaveHip::sync();
-    for (int i = WaveHip::lane(); i < width; i += 64) orders[(int64_t)k * width + i] = i < n ? out[i] : -1;
-    WaveHip::sync();
-  }
-}
-
 // per-job arrival/completion times and state (JobRec/JobTimes in the hot block) -> [num_envs][job_cap]
 __global__ __launch_bounds__(64) void k_job_times(const Params* __restrict__ P, const uint8_t* state,
                                                   double* ta, double* tc, int32_t* st) {
@@ -180,6 +146,14 @@ static KernelSet pick_kernels(const Params& p) {
   }
   if (bench_shape(p)) return p.L.stage_cap == 900 ? kernels_bench900() : kernels_bench();
   return kernels_lds();
+}
+static DecimaRolloutSet pick_decima(const Params& p) {
+#if SSIM_WITH_WINDOWED
+  if (!p.O.lds_resident && decima_shape(p) && windowed_enabled()) return decima_rollout_win50();
+#endif
+  return p.O.lds_resident                          ? decima_rollout_lds()
+         : !decima_shape(p) || generic_forced()   ? decima_rollout_hbm()
+                                                  : decima_rollout_hbm50();
 }
 static StepFn pick_step(const Params& p) { return pick_kernels(p).step; }
 static RolloutFn pick_rollout(const Params& p, bool warmup = false) {
@@ -246,9 +220,21 @@ static int lds_opt_in(const void* fn, int64_t lds) {
   return rc;
 }
 
+// Compute units of the current device (the layout's LDS-residency threshold, layout.h compute_layout); a whole MI355X
+// when there is no device (host-only use of ssim_layout_for).
+static int64_t device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      n <= 0) {
+    (void)hipGetLastError();  // (clear the sticky error of a host without a device)
+    return kChipCus;
+  }
+  return n;
+}
+
 extern "C" int ssim_layout_for(const ssim_config* cfg, ssim_layout* out) {
   StateOffsets O;
-  if (cfg == nullptr || out == nullptr || !compute_layout(*cfg, out, &O))
+  if (cfg == nullptr || out == nullptr || !compute_layout(*cfg, out, &O, device_cus()))
     return set_err(SSIM_E_ARG, "ssim_layout_for: invalid config");
   return SSIM_OK;
 }
@@ -259,7 +245,7 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
       reset_arena == nullptr || out == nullptr)
     return set_err(SSIM_E_ARG, "ssim_create: null argument");
   ssim_handle* h = new ssim_handle();
-  if (!compute_layout(*cfg, &h->params.L, &h->params.O)) {
+  if (!compute_layout(*cfg, &h->params.L, &h->params.O, device_cus())) {
     delete h;
     return set_err(SSIM_E_ARG, "ssim_create: invalid config");
   }
@@ -479,15 +465,54 @@ extern "C" int ssim_job_times(ssim_handle* h, double* t_arrival, double* t_compl
   return hip_check(hipGetLastError(), "k_job_times launch");
 }
 
-extern "C" int ssim_debug_set_trace(ssim_handle* h, const int32_t* ops, int32_t n_ops, int32_t width, int32_t* orders,
-                                    void* stream) {
+// The set KAT (tests/test_gpu_sets.py) through the engine instantiation a launch on this handle runs: variant
+// SSIM_DEBUG_ENGINE the step / rollout kernels' (pick_kernels), SSIM_DEBUG_DECIMA the persistent Decima rollout's
+// (pick_decima), SSIM_DEBUG_KAT_BAD the test-only known-bad page assembly (N = 100 / J = 200, HBM-resident layouts).
+static const char* debug_variant(const ssim_handle* h, int32_t variant, SetTraceFn* fn) {
+  if (variant == SSIM_DEBUG_ENGINE) {
+    const KernelSet k = pick_kernels(h->params);
+    *fn = k.set_trace;
+    return k.name;
+  }
+  if (variant == SSIM_DEBUG_DECIMA) {
+    const DecimaRolloutSet k = pick_decima(h->params);
+    *fn = k.set_trace;
+    return k.name;
+  }
+  if (variant == SSIM_DEBUG_KAT_BAD && large_shape(h->params) && !h->params.O.lds_resident) {
+    *fn = set_trace_kat_bad();
+    return "kat_bad_page";
+  }
+  *fn = nullptr;
+  return nullptr;
+}
+
+extern "C" const char* ssim_debug_kernel_name(const ssim_handle* h, int32_t variant) {
+  SetTraceFn fn;
+  const char* n = h != nullptr ? debug_variant(h, variant, &fn) : nullptr;
+  return n != nullptr ? n : "";
+}
+
+extern "C" int ssim_debug_set_trace_ex(ssim_handle* h, const int32_t* ops, int32_t n_ops, int32_t width,
+                                       int32_t* orders, int32_t variant, void* stream) {
   if (h == nullptr || ops == nullptr || orders == nullptr || n_ops < 0 || width <= 0)
     return set_err(SSIM_E_ARG, "ssim_debug_set_trace: bad argument");
   if (h->params.L.num_executors > 127 || h->params.L.job_cap < 1)
     return set_err(SSIM_E_ARG, "ssim_debug_set_trace: needs 1..127 executors and a job cap >= 1");
-  hipLaunchKernelGGL(k_debug_set_trace, dim3(1), dim3(64), (size_t)h->params.L.scratch_bytes, (hipStream_t)stream,
-                     dparams(h), h->state, h->obs, ops, n_ops, width, orders);
-  return hip_check(hipGetLastError(), "k_debug_set_trace launch");
+  SetTraceFn fn = nullptr;
+  if (debug_variant(h, variant, &fn) == nullptr)
+    return set_err(SSIM_E_ARG, "ssim_debug_set_trace: variant %d does not apply to this layout", variant);
+  const int64_t lds = h->params.O.lds_bytes;
+  const int rc = lds_opt_in((const void*)fn, lds);
+  if (rc != SSIM_OK) return rc;
+  hipLaunchKernelGGL(fn, dim3(1), dim3(64), (size_t)lds, (hipStream_t)stream, dparams(h), h->state, h->obs, ops, n_ops,
+                     width, orders);
+  return hip_check(hipGetLastError(), "k_set_trace launch");
+}
+
+extern "C" int ssim_debug_set_trace(ssim_handle* h, const int32_t* ops, int32_t n_ops, int32_t width, int32_t* orders,
+                                    void* stream) {
+  return ssim_debug_set_trace_ex(h, ops, n_ops, width, orders, SSIM_DEBUG_ENGINE, stream);
 }
 
 extern "C" int ssim_decima_features(ssim_handle* h, float num_tasks_scale, float work_scale, float* node_feats,
@@ -569,7 +594,7 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
   if (num_params != kDecimaParams)
     return set_err(SSIM_E_ARG, "ssim_decima_rollout: %d parameters, the fused kernel implements the "
                    "decima_tpch.yaml architecture (%d)", num_params, kDecimaParams);
-  if ((flags & ~(SSIM_ROLLOUT_AUTORESET | SSIM_ROLLOUT_PREEMPT | SSIM_ROLLOUT_WARMUP)) != 0)
+  if ((flags & ~(SSIM_ROLLOUT_AUTORESET | SSIM_ROLLOUT_PREEMPT | SSIM_ROLLOUT_WARMUP | SSIM_ROLLOUT_TEST_REJECT)) != 0)
     return set_err(SSIM_E_ARG, "ssim_decima_rollout: unknown flags 0x%x", flags);
   if ((flags & SSIM_ROLLOUT_PREEMPT) && total_decisions <= 0)
     return set_err(SSIM_E_ARG, "ssim_decima_rollout: SSIM_ROLLOUT_PREEMPT needs a decision budget");
@@ -600,12 +625,7 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
       return set_err(SSIM_E_ARG, "ssim_decima_rollout: incomplete sample arena");
     a.smp = sm;
   }
-  DecimaRolloutSet ks = h->params.O.lds_resident   ? decima_rollout_lds()
-                       : !decima_shape(h->params) || generic_forced() ? decima_rollout_hbm()
-                                                  : decima_rollout_hbm50();
-#if SSIM_WITH_WINDOWED
-  if (!h->params.O.lds_resident && decima_shape(h->params) && windowed_enabled()) ks = decima_rollout_win50();
-#endif
+  const DecimaRolloutSet ks = pick_decima(h->params);
   const DecimaRolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
   const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
   const int rc = lds_opt_in((const void*)fn, lds);

@@ -51,6 +51,10 @@ def lib() -> ct.CDLL:
     L.ssim_build_id.restype = ct.c_char_p
     L.ssim_debug_set_trace.argtypes = [vp, vp, i32, i32, vp, vp]
     L.ssim_debug_set_trace.restype = ct.c_int
+    L.ssim_debug_set_trace_ex.argtypes = [vp, vp, i32, i32, vp, i32, vp]
+    L.ssim_debug_set_trace_ex.restype = ct.c_int
+    L.ssim_debug_kernel_name.argtypes = [vp, i32]
+    L.ssim_debug_kernel_name.restype = ct.c_char_p
     L.ssim_linear_fwd.argtypes = [vp, vp, vp, vp, ct.c_int64, i32, i32, i32, vp]
     L.ssim_linear_fwd.restype = ct.c_int
     L.ssim_linear_wgrad_parts.argtypes = [ct.c_int64]
@@ -74,7 +78,8 @@ EXPORTED_SYMBOLS = ["ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_rese
                     "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
                     "ssim_job_times",
                     "ssim_decima_features", "ssim_decima_policy", "ssim_decima_workspace_bytes", "ssim_decima_rollout",
-                    "ssim_last_error", "ssim_build_id", "ssim_debug_set_trace", "ssim_linear_fwd",
+                    "ssim_last_error", "ssim_build_id", "ssim_debug_set_trace", "ssim_debug_set_trace_ex",
+                    "ssim_debug_kernel_name", "ssim_linear_fwd",
                     "ssim_linear_wgrad_parts", "ssim_linear_wgrad"]
 
 

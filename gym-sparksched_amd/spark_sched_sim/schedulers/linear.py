@@ -72,9 +72,20 @@ class _LinearFn(torch.autograd.Function):
 class HipLinear(nn.Linear):
     """nn.Linear (same parameters); f32 device inputs of widths <= 64 run on csrc/k_linear.hip."""
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def _kernel_ok(self, x: torch.Tensor) -> bool:
+        """The kernels read raw f32 pointers on x's device: anything else (CPU tensors, other dtypes, parameters on
+        another device, widths > 64) takes F.linear, which raises torch's own errors for mismatches."""
         if not x.is_cuda or x.dtype != torch.float32 or self.in_features > _MAX or self.out_features > _MAX:
+            return False
+        w, b = self.weight, self.bias
+        if w.dtype != torch.float32 or w.device != x.device:
+            return False
+        return b is None or (b.dtype == torch.float32 and b.device == x.device)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not self._kernel_ok(x):
             return F.linear(x, self.weight, self.bias)
         lead = x.shape[:-1]
-        y = _LinearFn.apply(x.reshape(-1, self.in_features), self.weight, self.bias)
+        with torch.cuda.device(x.device):
+            y = _LinearFn.apply(x.reshape(-1, self.in_features), self.weight, self.bias)
         return y.reshape(*lead, self.out_features)

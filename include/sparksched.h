@@ -207,6 +207,9 @@ int ssim_rollout(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps,
 /* Same rollout, launched under the kernel symbol k_rollout_warmup instead of k_rollout, so a profiler's per-kernel
  * statistics can tell launches that are not measured (a benchmark's pre-roll and warm-up) from measured ones. */
 #define SSIM_ROLLOUT_WARMUP 0x4
+/* ssim_decima_rollout only, a test hook: the launch's first decision of every env asks for N + 1 executors, an action
+ * the env refuses (the env freezes with SSIM_ERR_INVARIANT and the sample recorded for it is dropped). */
+#define SSIM_ROLLOUT_TEST_REJECT 0x8
 int ssim_rollout_ex(ssim_handle* h, int32_t kind, uint64_t seed, int32_t num_steps, int32_t flags,
                     const double* time_limits, int32_t* action_log, void* stream);
 
@@ -314,6 +317,19 @@ const char* ssim_last_error(void);
  * needs 1..127 executors. */
 int ssim_debug_set_trace(ssim_handle* h, const int32_t* ops, int32_t n_ops, int32_t width, int32_t* orders,
                          void* stream);
+/* The same trace through a chosen engine instantiation, compiled in the translation unit (with the flags) of the kernels
+ * a launch on this handle runs: SSIM_DEBUG_ENGINE = ssim_step / ssim_rollout*'s (what ssim_debug_set_trace runs),
+ * SSIM_DEBUG_DECIMA = ssim_decima_rollout's, SSIM_DEBUG_KAT_BAD = a test-only instantiation that reproduces the effect
+ * of the ROCm 7.2 page-assembly miscompile the engine works around (N = 100 / job cap 200, HBM-resident layouts only:
+ * the KAT must fail on it). SSIM_E_ARG when the variant does not apply to the handle's layout. */
+#define SSIM_DEBUG_ENGINE 0
+#define SSIM_DEBUG_DECIMA 1
+#define SSIM_DEBUG_KAT_BAD 2
+int ssim_debug_set_trace_ex(ssim_handle* h, const int32_t* ops, int32_t n_ops, int32_t width, int32_t* orders,
+                            int32_t variant, void* stream);
+/* Name of the kernel translation unit a variant selects for this handle ("hbm_n100", "bench900", "dr_hbm50", ...; ""
+ * when the variant does not apply). */
+const char* ssim_debug_kernel_name(const ssim_handle* h, int32_t variant);
 
 /* The PPO learner's small dense layers (widths <= 64: the Decima MLPs) on the device, replacing the nn.Linear GEMMs
  * of trainers/ppo.py's evaluate_actions passes (reference: schedulers/decima/utils.py:51-70 make_mlp, trained by

@@ -92,29 +92,88 @@ def test_cpython_reference_grows_and_churns_tables():
     assert max(sizes) >= 77 and sum(1 for c, _, _ in ops if c == 1) > 200 and sum(1 for c, _, _ in ops if c == 2) > 50
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("n_exec,traces,n_ops", CASES)
-def test_device_sets_match_cpython(gpu_device, dataset, n_exec, traces, n_ops):
+# The shipped shape-specialised instantiations (ssim_debug_set_trace_ex runs the KAT through the engine template
+# instantiation of the translation unit a launch on the handle selects, compiled there with that unit's flags): the
+# configs[1] LDS-resident kernel (stage cap 900), its HBM-resident form for large batches, the configs[2] / [4] engine
+# and Decima rollout units (N = 50) and the configs[3] unit (N = 100), where round 4's ROCm i64 miscompile hid from the
+# generic kernel. (executors, job cap, config flags, variant, expected unit, traces, ops per trace)
+_HBM, _ENG, _DEC = 1, 0, 1  # _abi.SSIM_CFG_FORCE_HBM, SSIM_DEBUG_ENGINE, SSIM_DEBUG_DECIMA
+SHIPPED = [(10, 50, 0, _ENG, "bench900", 8, 400), (10, 50, _HBM, _ENG, "hbm_n10", 8, 400),
+           (50, 200, _HBM, _ENG, "hbm_n50", 10, 600), (50, 200, _HBM, _DEC, "dr_hbm50", 10, 600),
+           (100, 200, _HBM, _ENG, "hbm_n100", 12, 900)]
+
+
+def _run_traces(eng, n_exec, traces, n_ops, variant, stop_at_first=False):
+    """Runs `traces` random traces through `variant`; returns the mismatches (trace, op, device, CPython)."""
     import torch
 
     from spark_sched_sim import native
-    from spark_sched_sim.engine import DeviceEngine
 
-    cfg = dict(num_executors=n_exec, job_arrival_cap=2, job_arrival_rate=4.0e-5, moving_delay=2000.0,
-               warmup_delay=1000.0)
-    eng = DeviceEngine(cfg, 1, dataset, device=gpu_device)
-    width = n_exec + 1
+    width, bad = n_exec + 1, []
     for t in range(traces):
         rng = np.random.default_rng([n_exec, t])
         ops = random_ops(rng, n_exec, n_ops)
         want = cpython_orders(ops)
         dev_ops = torch.from_numpy(encode(ops, n_exec)).to(eng.device)
         orders = torch.full((len(ops), width), -2, dtype=torch.int32, device=eng.device)
-        native.check(native.lib().ssim_debug_set_trace(eng.handle, dev_ops.data_ptr(), len(ops), width,
-                                                       orders.data_ptr(), eng._stream()), "ssim_debug_set_trace")
+        native.check(native.lib().ssim_debug_set_trace_ex(eng.handle, dev_ops.data_ptr(), len(ops), width,
+                                                          orders.data_ptr(), variant, eng._stream()),
+                     "ssim_debug_set_trace_ex")
         got = orders.cpu().numpy()
         for k, w in enumerate(want):
             row = got[k]
             g = row[row >= 0].tolist()
-            assert g == w, (f"N={n_exec} trace {t} op {k} {ops[k][:2]}: device {g} vs CPython {w}")
+            if g != w:
+                bad.append((t, k, g, w))
+                if stop_at_first:
+                    return bad
+    return bad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_exec,traces,n_ops", CASES)
+def test_device_sets_match_cpython(gpu_device, dataset, n_exec, traces, n_ops):
+    """Small-batch layouts (job cap 2, one env): the generic LDS-resident unit."""
+    from spark_sched_sim.engine import DeviceEngine
+
+    cfg = dict(num_executors=n_exec, job_arrival_cap=2, job_arrival_rate=4.0e-5, moving_delay=2000.0,
+               warmup_delay=1000.0)
+    eng = DeviceEngine(cfg, 1, dataset, device=gpu_device)
+    bad = _run_traces(eng, n_exec, traces, n_ops, _ENG, stop_at_first=True)
+    assert not bad, f"N={n_exec} trace {bad[0][0]} op {bad[0][1]}: device {bad[0][2]} vs CPython {bad[0][3]}"
     eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_exec,job_cap,flags,variant,unit,traces,n_ops", SHIPPED)
+def test_shipped_instantiations_sets_match_cpython(gpu_device, dataset, n_exec, job_cap, flags, variant, unit, traces,
+                                                   n_ops):
+    from spark_sched_sim import native
+    from spark_sched_sim.engine import DeviceEngine
+
+    cfg = dict(num_executors=n_exec, job_arrival_cap=job_cap, job_arrival_rate=4.0e-5, moving_delay=2000.0,
+               warmup_delay=1000.0)
+    eng = DeviceEngine(cfg, 1, dataset, device=gpu_device, config_flags=flags)
+    ran = native.lib().ssim_debug_kernel_name(eng.handle, variant).decode()
+    assert ran == unit, f"the layout selects {ran!r}, expected the shipped unit {unit!r}"
+    bad = _run_traces(eng, n_exec, traces, n_ops, variant, stop_at_first=True)
+    assert not bad, f"{unit} N={n_exec} trace {bad[0][0]} op {bad[0][1]}: device {bad[0][2]} vs CPython {bad[0][3]}"
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_known_bad_page_assembly_fails_the_kat(gpu_device, dataset):
+    """Regression guard: the N = 100 instantiation on a test-only wave type that reproduces round 4's miscompile
+    (engine.h KatBadPage: a clean-insert table rebuilt with key 0 in slot 256) must fail the same KAT
+    the shipped unit passes, so the KAT has the power to catch that class of error."""
+    from spark_sched_sim import native
+    from spark_sched_sim.engine import DeviceEngine
+
+    cfg = dict(num_executors=100, job_arrival_cap=200, job_arrival_rate=4.0e-5, moving_delay=2000.0,
+               warmup_delay=1000.0)
+    eng = DeviceEngine(cfg, 1, dataset, device=gpu_device, config_flags=_HBM)
+    assert native.lib().ssim_debug_kernel_name(eng.handle, 2).decode() == "kat_bad_page"
+    bad = _run_traces(eng, 100, 4, 900, 2, stop_at_first=True)
+    assert bad, "the known-bad page assembly passed the KAT: the KAT cannot see the miscompile it guards against"
+    eng.close()
+

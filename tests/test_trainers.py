@@ -672,3 +672,35 @@ def test_arena_grows_the_region_that_overflowed():
     arena.grow(cur)
     assert arena.caps == [16, 1 << 17, 1 << 10, 64], arena.caps
     assert arena.nodes.shape[1] == 1 << 17 and not (arena.cursor[:, _abi.CUR_FULL:] != 0).any()
+
+
+@pytest.mark.gpu
+def test_decima_rejected_action_leaves_no_sample(gpu_device, dataset):
+    """An action the env refuses (SSIM_ROLLOUT_TEST_REJECT: the launch's first decision asks for N + 1 executors,
+    spark_sched_sim.py:276-277's ValueError) freezes the env with SSIM_ERR_INVARIANT and takes the sample the policy
+    recorded for it, with its observation rows, back off the arena: the cursors end where the previous launch left
+    them, so no recorded sample holds an action the env did not take (DecimaPolicy::rejected)."""
+    from spark_sched_sim import _abi
+    from spark_sched_sim.engine import DeviceEngine
+    from spark_sched_sim.schedulers.decima import DecimaScheduler
+    from spark_sched_sim.trainers import DECIMA_TPCH
+    from spark_sched_sim.trainers.rollouts import DecimaSampleArena
+
+    env = {k: v for k, v in DECIMA_TPCH["env"].items() if k not in ("mean_time_limit", "dataset")}
+    B = 4
+    torch.manual_seed(5)
+    pol = DecimaScheduler(env["num_executors"]).to(gpu_device)
+    params = pol.packed_params(gpu_device)
+    eng = DeviceEngine(env, B, dataset, device=gpu_device)
+    eng.reset_sampled(_abi.SSIM_RESET_SEED, seeds=[501 + i for i in range(B)])
+    arena = DecimaSampleArena(B, eng.device, cap_samples=256, cap_nodes=1 << 14, cap_edges=1 << 14, cap_dags=1 << 11)
+    eng.decima_rollout(params, 9, 77, 5, samples=arena)  # 5 accepted decisions per env
+    before = arena.cursor.clone()
+    rec_before = arena.rec.clone()
+    assert before[:, 0].tolist() == [5] * B
+    eng.decima_rollout(params, 9, 77, 5, flags=_abi.SSIM_ROLLOUT_TEST_REJECT, samples=arena)
+    err = eng.views["counts"][:, _abi.OC_ERR].cpu().numpy()
+    assert ((err & _abi.SSIM_ERR_INVARIANT) != 0).all(), [hex(int(x)) for x in err]
+    assert torch.equal(arena.cursor[:, :4], before[:, :4]), (arena.cursor[:, :4], before[:, :4])
+    for i in range(B):
+        assert torch.equal(arena.rec[i, :5], rec_before[i, :5])
