@@ -26,7 +26,7 @@ namespace ssim {
 constexpr int kDecimaFeatures = 5;   // env_wrapper.py:9
 constexpr int kDecimaMaxDepth = 32;  // edge_mask bits; DAG depth <= max_stages (checked at the ABI)
 
-// LDS scratch per env: level i32[S], parent-level bits u32[S], job of node i16[S]
+// LDS scratch per env: level i32[S], parent-level bits u32[S], job of node i16[S] (S: the node capacity)
 inline int64_t decima_scratch_bytes(int64_t stage_cap) { return align16(10 * stage_cap); }
 
 // Cross-lane ordering of the scratch updates. LDS scratch (k_decima): the wave's own ds operations are in order, a
@@ -47,10 +47,12 @@ struct DecimaView {
   const uint8_t* obs;
   int eid;
 
+  // scratch: decima_scratch_bytes(scap) bytes laid out for scap nodes (>= the observation's; default the stage cap)
   template <bool kGlobal = false>
   __device__ __forceinline__ void run(float num_tasks_scale, float work_scale, uint8_t* scratch, float* feats,
-                                      int32_t* ccap, uint32_t* emask, int32_t* depth_out) const {
+                                      int32_t* ccap, uint32_t* emask, int32_t* depth_out, int scap = 0) const {
     const int S = L.stage_cap, J = L.job_cap, E = L.edge_cap, N = L.num_executors;
+    const int SC = scap > 0 ? scap : S;
     const int32_t* cnt = reinterpret_cast<const int32_t*>(obs + L.ob_counts) + (int64_t)eid * SSIM_NUM_COUNTS;
     const int n = W::uni(cnt[SSIM_OC_NUM_NODES]), ne = W::uni(cnt[SSIM_OC_NUM_EDGES]);
     const int nj = W::uni(cnt[SSIM_OC_NUM_JOBS]), comm = W::uni(cnt[SSIM_OC_COMMITTABLE]);
@@ -60,8 +62,8 @@ struct DecimaView {
     const int32_t* ptr = reinterpret_cast<const int32_t*>(obs + L.ob_dag_ptr) + (int64_t)eid * (J + 1);
     const int32_t* sup = reinterpret_cast<const int32_t*>(obs + L.ob_supplies) + (int64_t)eid * J;
     int32_t* lev = reinterpret_cast<int32_t*>(scratch);
-    uint32_t* plm = reinterpret_cast<uint32_t*>(scratch + 4 * (int64_t)S);
-    int16_t* job_of = reinterpret_cast<int16_t*>(scratch + 8 * (int64_t)S);
+    uint32_t* plm = reinterpret_cast<uint32_t*>(scratch + 4 * (int64_t)SC);
+    int16_t* job_of = reinterpret_cast<int16_t*>(scratch + 8 * (int64_t)SC);
     float* f = feats + (int64_t)eid * S * kDecimaFeatures;
     int32_t* cc = ccap + (int64_t)eid * J;
     uint32_t* em = emask + (int64_t)eid * E;

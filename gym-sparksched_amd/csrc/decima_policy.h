@@ -49,6 +49,7 @@ constexpr int kOffExec = kOffStage + MlpStage::kParams;
 constexpr int kDecimaParams = kOffExec + MlpExec::kParams;  // 20802
 
 constexpr int64_t kDecimaPolicyLdsMax = 160 * 1024;  // gfx950 LDS per workgroup (opt-in above 64 KB)
+constexpr int kDpLdsDags = 16;  // DAG rows of the persistent rollout's LDS plan (observations with more take the global)
 
 // Plan per env: h_init, h, agg, msg [cap][16] f32, score f32 [cap], node->DAG i16 [cap], flags u8 [cap] (bit0
 // has-child), level marks u8 [cap] (bit0 child of a level edge, bit1 parent of one), compacted node lists i16 [cap]
@@ -97,117 +98,210 @@ __device__ __forceinline__ float dp_leaky(float v) { return v >= 0.0f ? v : 0.2f
 // accumulate: a k-ordered fmaf chain per output, no reduced precision). Lane l works on row l & 15; lane quarter
 // q = l >> 4 supplies input k = 4s + q of step s. The accumulator of a 16-unit tile holds, in register r of lane l,
 // unit 4q + r of row l & 15, and a hidden layer takes the previous layer's accumulators as its B operand (step r of
-// tile t' reads unit 16t' + 4q + r: the input order is permuted to match), so layers chain in registers. The weights
-// (ssim_decima_policy's layout: the module's parameters() in order, nn.Linear [out][in] weights) are gathered per
-// step as the A operand through one per-lane pointer per output tile (immediate step offsets). 16-row tiles fit the
-// observations of the Decima workloads (~16 nodes per decision at J=200); a per-lane MLP (one row per lane, weights
-// as scalar operands) left most lanes idle there and waited on a scalar load per weight row.
+// tile t' reads unit 16t' + 4q + r: the input order is permuted to match), so layers chain in registers. 16-row tiles
+// fit the observations of the Decima workloads (~16 nodes per decision at J=200); a per-lane MLP (one row per lane,
+// weights as scalar operands) left most lanes idle there and waited on a scalar load per weight row.
+//
+// The weights (A operands) come from a PACKED copy of the parameters in the order the matrix cores consume them
+// (DpPacked below; k_decima_pack builds it from the module's parameters() at each launch): per output tile and group
+// of four steps, each lane's four A values are one aligned 16-B word, and the 64 lanes' words are contiguous. A group
+// of four MFMA steps per output tile is then ONE 16-B load per lane (ds_read_b128 from the LDS copy of the persistent
+// rollout, a coalesced 1-KB global_load_dwordx4 otherwise) at a compile-time offset from one lane-offset register,
+// instead of a 4-B gather per step through a 64-bit pointer per tile from 16 different weight rows.
 typedef float dp_f32x4 __attribute__((ext_vector_type(4)));
-// Steps per scheduling group: a group's operand loads are issued together and not hoisted past the group before
-// (sched_barrier), which bounds the registers in flight.
-#ifndef SSIM_DP_GROUP
-#define SSIM_DP_GROUP 4
-#endif
-constexpr int kDpGroup = SSIM_DP_GROUP;
 
+// Packed layout of one MLP (units of 16 B): W0 [T1][G0][64 lanes] (lane l, word j of group g, tile t: W0[16t + (l &
+// 15)][16g + 4j + (l >> 4)], zero past IN), b0, W1 [T2][T1][64] (word r of group t': W1[16t + (l & 15)][16t' + 4(l >>
+// 4) + r]), b1, then W2 as W1 for 16 outputs, or natural for one output (the score MLPs' last layer runs on the VALU),
+// and b2.
+template <int IN, int H1, int H2, int OUT>
+struct Mlp3P {
+  static constexpr int G0 = (IN + 15) / 16, T1 = H1 / 16, T2 = H2 / 16;
+  static constexpr int kW0 = 0;
+  static constexpr int kB0 = kW0 + T1 * G0 * 64;
+  static constexpr int kW1 = kB0 + H1 / 4;
+  static constexpr int kB1 = kW1 + T2 * T1 * 64;
+  static constexpr int kW2 = kB1 + H2 / 4;
+  static constexpr int kB2 = kW2 + (OUT == 16 ? T2 * 64 : H2 / 4);
+  static constexpr int kSize = kB2 + (OUT + 3) / 4;
+  // Natural (nn.Linear, parameters() order) index of packed float f, -1 for a zero pad.
+  __host__ __device__ static int src(int f) {
+    const int oB0 = H1 * IN, oW1 = oB0 + H1, oB1 = oW1 + H2 * H1, oW2 = oB1 + H2, oB2 = oW2 + OUT * H2;
+    if (f < 4 * kB0) {
+      const int j = f & 3, l = (f >> 2) & 63, tg = f >> 8, t = tg / G0, g = tg % G0;
+      const int k = 16 * g + 4 * j + (l >> 4);
+      return k < IN ? (16 * t + (l & 15)) * IN + k : -1;
+    }
+    if (f < 4 * kW1) return oB0 + (f - 4 * kB0);
+    if (f < 4 * kB1) {
+      const int u = f - 4 * kW1, r = u & 3, l = (u >> 2) & 63, tt = u >> 8, t = tt / T1, tp = tt % T1;
+      return oW1 + (16 * t + (l & 15)) * H1 + 16 * tp + 4 * (l >> 4) + r;
+    }
+    if (f < 4 * kW2) return oB1 + (f - 4 * kB1);
+    if (f < 4 * kB2) {
+      const int u = f - 4 * kW2;
+      if (OUT != 16) return oW2 + u;
+      const int r = u & 3, l = (u >> 2) & 63, tp = u >> 8;
+      return oW2 + (l & 15) * H2 + 16 * tp + 4 * (l >> 4) + r;
+    }
+    const int u = f - 4 * kB2;
+    return u < OUT ? oB2 + u : -1;
+  }
+};
+using PPrep = Mlp3P<kDecimaFeatures, 32, 16, kDpEmb>;
+using PMsg = Mlp3P<kDpEmb, 32, 16, kDpEmb>;
+using PDag = Mlp3P<kDecimaFeatures + kDpEmb, 32, 16, kDpEmb>;
+using PStage = Mlp3P<kDecimaFeatures + 3 * kDpEmb, 64, 64, 1>;
+using PExec = Mlp3P<3 + 2 * kDpEmb + 1, 64, 64, 1>;
+// packed MLP bases (16-B units), in parameters() order
+constexpr int kPPrep = 0;
+constexpr int kPMsg = kPPrep + PPrep::kSize;
+constexpr int kPUpd = kPMsg + PMsg::kSize;
+constexpr int kPDag = kPUpd + PMsg::kSize;
+constexpr int kPGlob = kPDag + PDag::kSize;
+constexpr int kPStage = kPGlob + PMsg::kSize;
+constexpr int kPExec = kPStage + PStage::kSize;
+constexpr int kDpPacked = kPExec + PExec::kSize;           // 16-B units
+constexpr int64_t kDpPackedBytes = 16 * (int64_t)kDpPacked;  // ~92 KB
+// Natural index of packed float f of the whole policy (k_decima_pack), -1 = zero
+__host__ __device__ inline int dp_pack_src(int f) {
+  if (f < 4 * kPMsg) return kOffPrep + PPrep::src(f - 4 * kPPrep);
+  int r;
+  if (f < 4 * kPUpd) return (r = PMsg::src(f - 4 * kPMsg)) < 0 ? -1 : kOffMsg + r;
+  if (f < 4 * kPDag) return (r = PMsg::src(f - 4 * kPUpd)) < 0 ? -1 : kOffUpd + r;
+  if (f < 4 * kPGlob) return (r = PDag::src(f - 4 * kPDag)) < 0 ? -1 : kOffDag + r;
+  if (f < 4 * kPStage) return (r = PMsg::src(f - 4 * kPGlob)) < 0 ? -1 : kOffGlob + r;
+  if (f < 4 * kPExec) return (r = PStage::src(f - 4 * kPStage)) < 0 ? -1 : kOffStage + r;
+  return (r = PExec::src(f - 4 * kPExec)) < 0 ? -1 : kOffExec + r;
+}
+
+// Weight sources: the packed copy in global memory, or its LDS copy (the persistent rollout's workgroups stage it).
+// grp(o): this lane's 16-B word of the group at o (16-B units); vec(o): the word at o (bias / last-layer vectors).
+struct DpWGlobal {
+  const dp_f32x4* p;
+  __device__ __forceinline__ dp_f32x4 grp(int o) const { return p[o + (int)__lane_id()]; }
+  __device__ __forceinline__ dp_f32x4 vec(int o) const { return p[o]; }
+};
+typedef __attribute__((address_space(3))) const dp_f32x4 dp_lds_f32x4;
+struct DpWLds {
+  dp_lds_f32x4* p;
+  __device__ __forceinline__ dp_f32x4 grp(int o) const { return p[o + (int)__lane_id()]; }
+  __device__ __forceinline__ dp_f32x4 vec(int o) const { return p[o]; }
+};
+// The weight pointer made opaque at each MLP call: every load derived from it is then loop-variant, so the compiler
+// does not hoist those of every MLP of the policy out of the tile loops to the function entry (where they were all
+// live at once: hundreds of VGPRs).
+__device__ __forceinline__ int64_t dp_zero() {  // an opaque 0 (offsets keep a pointer's address space; casts do not)
+  int64_t z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+__device__ __forceinline__ DpWGlobal dp_opaque(DpWGlobal w) {
+  w.p += dp_zero();
+  return w;
+}
+__device__ __forceinline__ DpWLds dp_opaque(DpWLds w) { return w; }
+// A row-source pointer made opaque at each tile: the per-lane addresses of a tile's inputs (one per MFMA step) then
+// depend on the tile and are not hoisted out of the tile loops, where they were all live at once (64-bit addresses and
+// exec masks per step: the policy spilled to scratch memory even as a standalone kernel).
+template <class T>
+__device__ __forceinline__ T* dp_opq(T* p) {
+  return p + dp_zero();
+}
+
+// tanh from the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32): 1 - 2 / (1 + e^(2|x|)), sign restored; below
+// |x| = 2^-12 tanh(x) = x to f32 precision (the subtraction would cancel there). Absolute error ~1e-7 against the
+// correctly rounded tanh: the score MLPs' two Tanh layers then stay within the 1e-5 the policy tests allow against the
+// PyTorch module, at ~8 instructions instead of the ~40 of the library tanhf (the dominant VALU cost of a score tile).
+__device__ __forceinline__ float dp_tanh(float x) {
+  const float a = __builtin_fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(a * 2.8853900817779268f);  // e^(2a) = 2^(2a log2 e)
+  const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+  return __builtin_copysignf(a < 0.000244140625f ? a : t, x);
+}
 template <bool kTanh>
 __device__ __forceinline__ float dp_act(float v) {
-  return kTanh ? tanhf(v) : dp_leaky(v);
+  return kTanh ? dp_tanh(v) : dp_leaky(v);
 }
 
-// first layer: inputs xin(k), k < IN, of this lane's row (natural k order); W0 [H][IN] row-major (nn.Linear), b [H].
-// Each output tile's weight operand is read through one per-lane pointer with the step as an immediate offset.
-template <int IN, int H, class XF>
-__device__ __forceinline__ void dp_layer_in(const float* __restrict__ W0, const float* __restrict__ b, XF xin,
-                                            dp_f32x4 (&y)[H / 16]) {
+// first layer: inputs xin(k), k < IN, of this lane's row (natural k order); packed W0 at ow, b0 at ob. One group of
+// four steps per iteration: a 16-B A word per output tile, then the steps (scheduling barrier between groups: a
+// group's loads are issued together and not hoisted past the group before, which bounds the registers in flight).
+template <int IN, int H, class WS, class XF>
+__device__ __forceinline__ void dp_layer_in(const WS& w, int ow, int ob, XF xin, dp_f32x4 (&y)[H / 16]) {
   static_assert(H % 16 == 0, "layer widths: multiples of 16");
-  constexpr int T = H / 16, STEPS = (IN + 3) / 4;
-  const int lane = (int)__lane_id(), q = lane >> 4, row = lane & 15;
-  const float* wl[T];
+  constexpr int T = H / 16, STEPS = (IN + 3) / 4, G = (IN + 15) / 16;
+  const int q = (int)__lane_id() >> 4;
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
-    wl[t] = W0 + (16 * t + row) * IN + q;
+  for (int t = 0; t < T; ++t) y[t] = w.vec(ob + 4 * t + q);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) y[t][r] = b[16 * t + 4 * q + r];
-  }
+  for (int g = 0; g < G; ++g) {
+    dp_f32x4 wa[T];
 #pragma unroll
-  for (int st = 0; st < STEPS; ++st) {
-    const bool kin = 4 * st + 3 < IN || 4 * st + q < IN;
-    const float xv = kin ? xin(4 * st + q) : 0.0f;
+    for (int t = 0; t < T; ++t) wa[t] = w.grp(ow + (t * G + g) * 64);
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const float wv = kin ? wl[t][4 * st] : 0.0f;
-      y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv, xv, y[t], 0, 0, 0);
+    for (int j = 0; j < 4; ++j) {
+      const int st = 4 * g + j;
+      if (st < STEPS) {
+        const bool kin = 4 * st + 3 < IN || 4 * st + q < IN;
+        const float xv = kin ? xin(4 * st + q) : 0.0f;
+#pragma unroll
+        for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][j], xv, y[t], 0, 0, 0);
+      }
     }
-    if ((st & (kDpGroup - 1)) == kDpGroup - 1) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
-// hidden / output layer from the previous layer's accumulators x (HP units, activated here); Wm [H][HP] row-major
-template <int HP, int H, bool kTanh>
-__device__ __forceinline__ void dp_layer_h(const float* __restrict__ Wm, const float* __restrict__ b,
-                                           const dp_f32x4 (&x)[HP / 16], dp_f32x4 (&y)[H / 16]) {
+// hidden / output layer from the previous layer's accumulators x (HP units, activated here); packed W at ow, b at ob
+template <int HP, int H, bool kTanh, class WS>
+__device__ __forceinline__ void dp_layer_h(const WS& w, int ow, int ob, const dp_f32x4 (&x)[HP / 16],
+                                           dp_f32x4 (&y)[H / 16]) {
   static_assert(H % 16 == 0 && HP % 16 == 0, "layer widths: multiples of 16");
   constexpr int T = H / 16, TP = HP / 16;
-  const int lane = (int)__lane_id(), q = lane >> 4, row = lane & 15;
-  const float* wl[T];
+  const int q = (int)__lane_id() >> 4;
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
-    wl[t] = Wm + (16 * t + row) * HP + 4 * q;
+  for (int t = 0; t < T; ++t) y[t] = w.vec(ob + 4 * t + q);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) y[t][r] = b[16 * t + 4 * q + r];
-  }
+  for (int tp = 0; tp < TP; ++tp) {
+    dp_f32x4 wa[T];
 #pragma unroll
-  for (int tp = 0; tp < TP; ++tp)
+    for (int t = 0; t < T; ++t) wa[t] = w.grp(ow + (t * TP + tp) * 64);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float xv = dp_act<kTanh>(x[tp][r]);
 #pragma unroll
-      for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wl[t][16 * tp + r], xv, y[t], 0, 0, 0);
-      if (((4 * tp + r) & (kDpGroup - 1)) == kDpGroup - 1) __builtin_amdgcn_sched_barrier(0);
+      for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][r], xv, y[t], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
-// The weight pointer made opaque at each MLP call: every lane pointer and bias load derived from it is then
-// loop-variant, so the compiler does not hoist those of every MLP of the policy out of the tile loops to the function
-// entry (where they were all live at once: hundreds of VGPRs).
-__device__ __forceinline__ const float* dp_opaque(const float* p) {
-  asm volatile("" : "+s"(p));
-  return p;
-}
-// 3-layer MLP with 16 outputs (the GNN MLPs, LeakyReLU(0.2) between layers): y register r of lane l = output
-// 4 (l >> 4) + r of row l & 15
-template <int IN, int H1, int H2, class XF>
-__device__ __forceinline__ void dp_mlp16(const float* __restrict__ p0, XF xin, dp_f32x4 (&y)[1]) {
-  const float* p = dp_opaque(p0);
-  const float* W0 = p;  // [H1][IN]
-  const float* b0 = W0 + H1 * IN;
-  const float* W1 = b0 + H1;  // [H2][H1]
-  const float* b1 = W1 + H2 * H1;
-  const float* W2 = b1 + H2;  // [16][H2]
-  const float* b2 = W2 + kDpEmb * H2;
+// 3-layer MLP with 16 outputs (the GNN MLPs, LeakyReLU(0.2) between layers) at packed base `pb`: y register r of lane
+// l = output 4 (l >> 4) + r of row l & 15
+template <int IN, int H1, int H2, class WS, class XF>
+__device__ __forceinline__ void dp_mlp16(const WS& w0, int pb, XF xin, dp_f32x4 (&y)[1]) {
+  using PL = Mlp3P<IN, H1, H2, kDpEmb>;
+  const WS w = dp_opaque(w0);
   dp_f32x4 a1[H1 / 16], a2[H2 / 16];
-  dp_layer_in<IN, H1>(W0, b0, xin, a1);
-  dp_layer_h<H1, H2, false>(W1, b1, a1, a2);
-  dp_layer_h<H2, kDpEmb, false>(W2, b2, a2, y);
+  dp_layer_in<IN, H1>(w, pb + PL::kW0, pb + PL::kB0, xin, a1);
+  dp_layer_h<H1, H2, false>(w, pb + PL::kW1, pb + PL::kB1, a1, a2);
+  dp_layer_h<H2, kDpEmb, false>(w, pb + PL::kW2, pb + PL::kB2, a2, y);
 }
 // 3-layer MLP with one output (the policy score MLPs, Tanh between layers): the score of row l & 15, in every quarter
-template <int IN, int H1, int H2, class XF>
-__device__ __forceinline__ float dp_mlp1(const float* __restrict__ p0, XF xin) {
-  const float* p = dp_opaque(p0);
-  const float* W0 = p;  // [H1][IN]
-  const float* b0 = W0 + H1 * IN;
-  const float* W1 = b0 + H1;  // [H2][H1]
-  const float* b1 = W1 + H2 * H1;
-  const float* W2 = b1 + H2;  // [1][H2]
-  const float* b2 = W2 + H2;
+template <int IN, int H1, int H2, class WS, class XF>
+__device__ __forceinline__ float dp_mlp1(const WS& w0, int pb, XF xin) {
+  using PL = Mlp3P<IN, H1, H2, 1>;
+  const WS w = dp_opaque(w0);
   dp_f32x4 a1[H1 / 16], a2[H2 / 16];
-  dp_layer_in<IN, H1>(W0, b0, xin, a1);
-  dp_layer_h<H1, H2, true>(W1, b1, a1, a2);
+  dp_layer_in<IN, H1>(w, pb + PL::kW0, pb + PL::kB0, xin, a1);
+  dp_layer_h<H1, H2, true>(w, pb + PL::kW1, pb + PL::kB1, a1, a2);
   const int q = (int)__lane_id() >> 4;
-  float part = q == 0 ? b2[0] : 0.0f;  // the last layer (H2 -> 1) on the VALU: this quarter's units, then all four
+  float part = q == 0 ? w.vec(pb + PL::kB2)[0] : 0.0f;  // the last layer (H2 -> 1) on the VALU: this quarter's units,
+#pragma unroll                                          // then all four
+  for (int t = 0; t < H2 / 16; ++t) {
+    const dp_f32x4 w2 = w.vec(pb + PL::kW2 + 4 * t + q);
 #pragma unroll
-  for (int t = 0; t < H2 / 16; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) part = __builtin_fmaf(W2[16 * t + 4 * q + r], tanhf(a2[t][r]), part);
+    for (int r = 0; r < 4; ++r) part = __builtin_fmaf(w2[r], dp_tanh(a2[t][r]), part);
+  }
   part += __shfl_xor(part, 16);
   return part + __shfl_xor(part, 32);
 }
@@ -257,13 +351,14 @@ __device__ __forceinline__ float dp_ld(const float* p) {
 // (k_decima_policy) or, with kGlobal, a per-env region of global memory (the persistent Decima rollout, whose
 // 16 waves per CU leave no LDS for a J=200 plan); the atomic accumulation phases then end with an agent-scope
 // fence (decima.h scratch_sync). `act` (optional) receives the action.
-template <bool kGlobal = false>
+template <bool kGlobal = false, class WS>
 __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, const uint8_t* __restrict__ obs,
                                          const float* __restrict__ feats, const int32_t* __restrict__ ccap,
                                          const uint32_t* __restrict__ emask, const int32_t* __restrict__ depth,
-                                         const float* __restrict__ Wt, int node_cap, uint64_t seed,
+                                         const WS& Wt, int node_cap, uint64_t seed,
                                          uint64_t counter, int eid, uint8_t* lds, const DecimaPolicyOut& o,
-                                         DpAction* act = nullptr, uint64_t* prof = nullptr) {
+                                         DpAction* act = nullptr, uint64_t* prof = nullptr,
+                                         int dag_cap = 0) {
   using W = WaveHip;
   // diagnostic -DSSIM_PROFILE builds: shader cycles per part and the observation's sizes into prof[0..9] (LDS, lane 0)
 #ifdef SSIM_PROFILE
@@ -313,7 +408,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   const uint32_t* em = emask + (int64_t)eid * E;
   const int levels = W::uni(depth[eid]) > 1 ? W::uni(depth[eid]) - 1 : 0;
 
-  const DpLds lo = dp_lds(node_cap, J);
+  const DpLds lo = dp_lds(node_cap, dag_cap > 0 ? dag_cap : J);  // (dag_cap: the caller guarantees nj <= dag_cap)
   float* hi = reinterpret_cast<float*>(lds + lo.hi);
   float* hh = reinterpret_cast<float*>(lds + lo.hh);
   float* agg = reinterpret_cast<float*>(lds + lo.agg);
@@ -352,7 +447,8 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     const int i = t0 + rl;
     const bool ok = i < n;
     dp_f32x4 v[1];
-    dp_mlp16<kDecimaFeatures, 32, 16>(Wt + kOffPrep, [&](int k) { return ok ? x[i * kDecimaFeatures + k] : 0.0f; }, v);
+    const float* xq = dp_opq(x);
+    dp_mlp16<kDecimaFeatures, 32, 16>(Wt, kPPrep, [&](int k) { return ok ? xq[i * kDecimaFeatures + k] : 0.0f; }, v);
     if (ok) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) hi[i * kDpEmb + 4 * hl + r] = v[0][r];
@@ -360,7 +456,8 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     if (levels > 0) {
       scratch_sync<W, kGlobal>();
       dp_f32x4 u[1];
-      dp_mlp16<kDpEmb, 32, 16>(Wt + kOffUpd, [&](int k) { return ok ? hi[i * kDpEmb + k] : 0.0f; }, u);
+      const float* hq = dp_opq(hi);
+      dp_mlp16<kDpEmb, 32, 16>(Wt, kPUpd, [&](int k) { return ok ? hq[i * kDpEmb + k] : 0.0f; }, u);
       if (ok) {
         const bool leaf = !(flag[i] & 1);
 #pragma unroll
@@ -407,7 +504,8 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
       const bool ok = t0 + rl < nc;
       const int c = ok ? clist[t0 + rl] : 0;
       dp_f32x4 m[1];
-      dp_mlp16<kDpEmb, 32, 16>(Wt + kOffMsg, [&](int k) { return ok ? hh[c * kDpEmb + k] : 0.0f; }, m);
+      const float* hq = dp_opq(hh);
+      dp_mlp16<kDpEmb, 32, 16>(Wt, kPMsg, [&](int k) { return ok ? hq[c * kDpEmb + k] : 0.0f; }, m);
       if (ok) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) msg[c * kDpEmb + 4 * hl + r] = m[0][r];
@@ -426,7 +524,8 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
       const bool ok = t0 + rl < np;
       const int i = ok ? plist[t0 + rl] : 0;
       dp_f32x4 u[1];
-      dp_mlp16<kDpEmb, 32, 16>(Wt + kOffUpd, [&](int k) { return ok ? dp_ld<kGlobal>(agg + i * kDpEmb + k) : 0.0f; },
+      const float* aq = dp_opq(agg);
+      dp_mlp16<kDpEmb, 32, 16>(Wt, kPUpd, [&](int k) { return ok ? dp_ld<kGlobal>(aq + i * kDpEmb + k) : 0.0f; },
                                u);
       if (ok) {
 #pragma unroll
@@ -444,8 +543,10 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     const int i = t0 + rl;
     const bool ok = i < n;
     dp_f32x4 v[1];
-    dp_mlp16<kDecimaFeatures + kDpEmb, 32, 16>(Wt + kOffDag, [&](int k) {
-      return !ok ? 0.0f : k < kDecimaFeatures ? x[i * kDecimaFeatures + k] : hh[i * kDpEmb + k - kDecimaFeatures];
+    const float* xq = dp_opq(x);
+    const float* hq = dp_opq(hh);
+    dp_mlp16<kDecimaFeatures + kDpEmb, 32, 16>(Wt, kPDag, [&](int k) {
+      return !ok ? 0.0f : k < kDecimaFeatures ? xq[i * kDecimaFeatures + k] : hq[i * kDpEmb + k - kDecimaFeatures];
     }, v);
     if (ok) {
       const int g = ndag[i];
@@ -458,7 +559,8 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     const int g = t0 + rl;
     const bool ok = g < nj;
     dp_f32x4 v[1];
-    dp_mlp16<kDpEmb, 32, 16>(Wt + kOffGlob, [&](int k) { return ok ? dp_ld<kGlobal>(hdag + g * kDpEmb + k) : 0.0f; },
+    const float* dq = dp_opq(hdag);
+    dp_mlp16<kDpEmb, 32, 16>(Wt, kPGlob, [&](int k) { return ok ? dp_ld<kGlobal>(dq + g * kDpEmb + k) : 0.0f; },
                              v);
     if (ok) {
 #pragma unroll
@@ -484,12 +586,16 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     const bool ok = t0 + rl < nsch;
     const int i = ok ? slist[t0 + rl] : 0;
     const int g = ndag[i];
-    const float sc = dp_mlp1<kDecimaFeatures + 3 * kDpEmb, 64, 64>(Wt + kOffStage, [&](int k) {
+    const float* xq = dp_opq(x);
+    const float* hq = dp_opq(hh);
+    const float* dq = dp_opq(hdag);
+    const float* gq = dp_opq(glob);
+    const float sc = dp_mlp1<kDecimaFeatures + 3 * kDpEmb, 64, 64>(Wt, kPStage, [&](int k) {
       return !ok                                   ? 0.0f
-             : k < kDecimaFeatures                 ? x[i * kDecimaFeatures + k]
-             : k < kDecimaFeatures + kDpEmb        ? hh[i * kDpEmb + k - kDecimaFeatures]
-             : k < kDecimaFeatures + 2 * kDpEmb    ? dp_ld<kGlobal>(hdag + g * kDpEmb + k - kDecimaFeatures - kDpEmb)
-                                                   : dp_ld<kGlobal>(glob + k - kDecimaFeatures - 2 * kDpEmb);
+             : k < kDecimaFeatures                 ? xq[i * kDecimaFeatures + k]
+             : k < kDecimaFeatures + kDpEmb        ? hq[i * kDpEmb + k - kDecimaFeatures]
+             : k < kDecimaFeatures + 2 * kDpEmb    ? dp_ld<kGlobal>(dq + g * kDpEmb + k - kDecimaFeatures - kDpEmb)
+                                                   : dp_ld<kGlobal>(gq + k - kDecimaFeatures - 2 * kDpEmb);
     });
     if (ok && hl == 0) {  // (every quarter holds the score; quarter 0 owns the row)
       score[i] = sc;
@@ -538,10 +644,13 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   for (int t0 = 0; t0 < cap; t0 += 16) {  // score of exec action k / N, k < cap, from [x_dag[:3], h_dag, h_glob, k/N]
     const int k = t0 + rl;
     const bool ok = k < cap;
-    const float sc = dp_mlp1<3 + 2 * kDpEmb + 1, 64, 64>(Wt + kOffExec, [&](int f) {
-      return f < 3             ? x[p0 * kDecimaFeatures + f]
-             : f < 3 + kDpEmb  ? dp_ld<kGlobal>(hdag + g * kDpEmb + f - 3)
-             : f < 3 + 2 * kDpEmb ? dp_ld<kGlobal>(glob + f - 3 - kDpEmb)
+    const float* xq = dp_opq(x);
+    const float* dq = dp_opq(hdag);
+    const float* gq = dp_opq(glob);
+    const float sc = dp_mlp1<3 + 2 * kDpEmb + 1, 64, 64>(Wt, kPExec, [&](int f) {
+      return f < 3             ? xq[p0 * kDecimaFeatures + f]
+             : f < 3 + kDpEmb  ? dp_ld<kGlobal>(dq + g * kDpEmb + f - 3)
+             : f < 3 + 2 * kDpEmb ? dp_ld<kGlobal>(gq + f - 3 - kDpEmb)
                                   : (float)k / (float)N;
     });
     if (ok && hl == 0) {

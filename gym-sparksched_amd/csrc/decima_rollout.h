@@ -8,8 +8,11 @@
 // per-env sample arena (the PPO learner's rollout buffer), then the step. No env waits for another; a launch runs
 // whole episodes (collection) or a shared decision budget (benchmark, SSIM_ROLLOUT_PREEMPT | AUTORESET).
 //
-// The features' scratch and the policy's activation plan live in a per-env region of global memory (the
-// workspace): at J = 200 a plan is ~0.7 MB, far above the LDS share of the 16 waves per CU a 4096-env batch runs.
+// The features' scratch and the policy's activation plan live in the wave's LDS share (the HBM-resident kernels run
+// 16 one-wave workgroups per CU: 10 KB each, overlaying the engine's per-operation scratch) for observations of up to
+// ~30 nodes and 16 DAGs (~9 in 10 decisions at J = 200), else in a per-env region of global memory (the workspace,
+// sized for the stage cap). The policy weights are packed per launch (k_decima_pack) into the operand order of the
+// matrix cores (decima_policy.h), a coalesced 16-B load per lane per four MFMA steps.
 // Sampling: counter-based Gumbel-max on (seed, env, counter + the env's decision index in its episode), plus the
 // episode number << 32 with auto-reset — the lockstep collector's stream (RolloutCollector: counter = base + k at
 // its k-th step), so both collectors draw the same actions for the same observations.
@@ -22,7 +25,8 @@
 // the feature outputs for all envs (the ssim_decima_features layout).
 struct DecimaWork {
   int64_t feat_scratch, plan, stride;  // per-env block
-  int64_t feats, ccap, emask, depth, total;  // absolute offsets of the [num_envs] feature arrays
+  int64_t feats, ccap, emask, depth;  // absolute offsets of the [num_envs] feature arrays
+  int64_t packed, total;              // the packed policy weights (kDpPackedBytes), then the end
 };
 inline DecimaWork decima_work(const ssim_layout& L) {
   DecimaWork w{};
@@ -38,20 +42,74 @@ inline DecimaWork decima_work(const ssim_layout& L) {
   o = align16(o + (int64_t)L.num_envs * L.edge_cap * 4);
   w.depth = o;
   o = align16(o + (int64_t)L.num_envs * 4);
-  w.total = o;
+  w.packed = (o + 255) & ~int64_t(255);
+  w.total = w.packed + kDpPackedBytes;
   return w;
 }
 
 struct DecimaRolloutArgs {
-  const float* weights;  // DecimaScheduler.packed_params()
+  const dp_f32x4* weights;  // the packed policy weights (decima_policy.h DpPacked; k_decima_pack of the parameters)
   uint8_t* work;         // decima_work(L).total bytes
   DecimaWork wl;
   float num_tasks_scale, work_scale;
   uint64_t seed, counter;
   int32_t autoreset;
   int32_t test_reject;      // SSIM_ROLLOUT_TEST_REJECT (test hook): the launch's first decision asks for N + 1 executors
+  // The LDS plan: an observation of at most plan_cap nodes runs the features' scratch and the policy's activations in
+  // the wave's LDS, at byte plan_off of its scratch block (what the layout would give the row map and the rest of the
+  // CU's share; the engine keeps its row map in the cold block). Larger ones use the env's global workspace.
+  int32_t plan_cap, plan_off;
   ssim_decima_samples smp;  // smp.rec == nullptr: no sample arena
 };
+
+// The Decima decision of one env's current observation: its features (decima.h) and the fused policy
+// (decima_policy.h), with the features' scratch and the policy's plan in the wave's LDS at byte `plan_lds` when the
+// observation has at most `plan_cap` nodes (0: in the env's global workspace: feat_scratch / plan). (Inlined: as a
+// call, the calling convention saved every live register around it, 1.2 KB per lane of scratch.)
+__device__ __forceinline__ DpAction decima_decide(
+    const Params* P0, const uint8_t* obs0, const dp_f32x4* weights0, uint8_t* feat_scratch0, uint8_t* plan0,
+    float* feats0, int32_t* ccap0, uint32_t* emask0, int32_t* depth0, float num_tasks_scale, float work_scale,
+    uint64_t seed, uint64_t ctr, int eid, int plan_cap, uint32_t plan_lds, uint64_t* pprof) {
+  using W = WaveHip;
+  const Params* P = (const Params*)(const SSIM_GLOBAL Params*)P0;
+  const uint8_t* obs = (const uint8_t*)(const SSIM_GLOBAL uint8_t*)obs0;
+  const dp_f32x4* weights = (const dp_f32x4*)(const SSIM_GLOBAL dp_f32x4*)weights0;
+  float* feats = (float*)(SSIM_GLOBAL float*)feats0;
+  int32_t* ccap = (int32_t*)(SSIM_GLOBAL int32_t*)ccap0;
+  uint32_t* emask = (uint32_t*)(SSIM_GLOBAL uint32_t*)emask0;
+  int32_t* depth = (int32_t*)(SSIM_GLOBAL int32_t*)depth0;
+  const ssim_layout& L = P->L;
+  const DecimaPolicyOut none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const DpWGlobal wts{weights};
+  DpAction act;
+#ifdef SSIM_PROFILE
+  uint64_t tp = W::clock();
+#endif
+#ifdef SSIM_DR_GLOBAL_ONLY
+  if (false) {  // (A/B builds: the global plan only)
+#else
+  if (plan_cap > 0) {  // the LDS plan (wave-local: cheap syncs, no global round trips per phase)
+#endif
+    uint8_t* pl = g_smem + plan_lds;
+    DecimaView<W>{L, obs, eid}.template run<false>(num_tasks_scale, work_scale, pl, feats, ccap, emask, depth,
+                                                   plan_cap);
+#ifdef SSIM_PROFILE
+    if (pprof != nullptr && W::lane() == 0) W::lds_add_u64(pprof - kPhDecParts + kPhDecFeat, W::clock() - tp);
+#endif
+    decima_policy_env<false>(P, obs, feats, ccap, emask, depth, wts, plan_cap, seed, ctr, eid, pl, none, &act, pprof,
+                             kDpLdsDags);
+  } else {  // the env's global workspace
+    uint8_t* fs = (uint8_t*)(SSIM_GLOBAL uint8_t*)feat_scratch0;
+    uint8_t* pg = (uint8_t*)(SSIM_GLOBAL uint8_t*)plan0;
+    DecimaView<W>{L, obs, eid}.template run<true>(num_tasks_scale, work_scale, fs, feats, ccap, emask, depth);
+#ifdef SSIM_PROFILE
+    if (pprof != nullptr && W::lane() == 0) W::lds_add_u64(pprof - kPhDecParts + kPhDecFeat, W::clock() - tp);
+#endif
+    decima_policy_env<true>(P, obs, feats, ccap, emask, depth, wts, L.stage_cap, seed, ctr, eid, pg, none, &act,
+                            pprof);
+  }
+  return act;
+}
 
 struct DecimaPolicy {
   const Params* P;
@@ -107,34 +165,32 @@ struct DecimaPolicy {
 #ifdef SSIM_PROFILE
     uint64_t tp = W::clock();
 #endif
+    SSIM_MARK("decima_act_begin");
     uint8_t* wk = a.work + (int64_t)eid * a.wl.stride;
     float* feats = reinterpret_cast<float*>(a.work + a.wl.feats);
     int32_t* ccap = reinterpret_cast<int32_t*>(a.work + a.wl.ccap);
     uint32_t* emask = reinterpret_cast<uint32_t*>(a.work + a.wl.emask);
     int32_t* depth = reinterpret_cast<int32_t*>(a.work + a.wl.depth);
-    DecimaView<W>{L, obs, eid}.template run<true>(a.num_tasks_scale, a.work_scale, wk + a.wl.feat_scratch, feats,
-                                                  ccap, emask, depth);
-#ifdef SSIM_PROFILE
-    s.prof_add(kPhDecFeat, W::clock() - tp);
-    tp = W::clock();
-#endif
     const uint64_t ctr = a.counter + (uint64_t)s.h.decisions + (a.autoreset ? (uint64_t)s.h.episode << 32 : 0ull);
-    DpAction act;
-    const DecimaPolicyOut none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 #ifdef SSIM_PROFILE
     uint64_t* pprof = s.prof + kPhDecParts;
 #else
     uint64_t* pprof = nullptr;
 #endif
-    decima_policy_env<true>(P, obs, feats, ccap, emask, depth, a.weights, L.stage_cap, a.seed, ctr, eid,
-                            wk + a.wl.plan, none, &act, pprof);
-    out->stage_idx = act.stage_idx;
-    out->num_exec = act.num_exec;
-    if (a.test_reject && k == 0) out->num_exec = L.num_executors + 1;  // (test hook: an action the env refuses)
+    const bool lds_plan = n <= a.plan_cap && nj <= kDpLdsDags;
+    SSIM_MARK("decima_policy_begin");
+    const DpAction act = decima_decide(P, obs, a.weights, wk + a.wl.feat_scratch, wk + a.wl.plan, feats, ccap, emask,
+                                       depth, a.num_tasks_scale, a.work_scale, a.seed, ctr, eid,
+                                       lds_plan ? a.plan_cap : 0,
+                                       (uint32_t)(s.scr + a.plan_off - g_smem), pprof);
+    SSIM_MARK("decima_policy_end");
 #ifdef SSIM_PROFILE
     s.prof_add(kPhDecPolicy, W::clock() - tp);
     tp = W::clock();
 #endif
+    out->stage_idx = act.stage_idx;
+    out->num_exec = act.num_exec;
+    if (a.test_reject && k == 0) out->num_exec = L.num_executors + 1;  // (test hook: an action the env refuses)
     if (sm.rec != nullptr) {  // the observation as the learner's DagBatch rows (schedulers/decima.py build_batch)
       const float* f = feats + (int64_t)eid * L.stage_cap * kDecimaFeatures;
       const float* nodes = reinterpret_cast<const float*>(obs + L.ob_nodes) + (int64_t)eid * L.stage_cap * 3;
@@ -189,6 +245,7 @@ struct DecimaPolicy {
 #ifdef SSIM_PROFILE
     s.prof_add(kPhDecRecord, W::clock() - tp);
 #endif
+    SSIM_MARK("decima_act_end");
     return true;
   }
   // the decision's reward (observe() wrote it to the obs arena) into its sample
@@ -240,7 +297,7 @@ __device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P
   a.test_reject = (flags & SSIM_ROLLOUT_TEST_REJECT) != 0;
   const DecimaPolicy pol{P, obs, a};
   rollout_body<kRes, kN, kJ, 0, DecimaPolicy, kWS, kWJ>(P, state, obs, pol, num_steps, flags, limits, reset, action_log,
-                                                       prof_out, budget, nullptr);
+                                                       prof_out, budget, nullptr, !kRes && kWS == 0);
 }
 // kWS / kWJ > 0: the windowed engine (kernels.h rollout_body), with kRes
 #define SSIM_DR_WAVES(kRes, kWS) ((kWS) > 0 ? SSIM_WIN_WAVES : (kRes) ? 1 : SSIM_DECIMA_ROLLOUT_WAVES)

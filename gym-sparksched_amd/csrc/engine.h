@@ -318,8 +318,10 @@ struct Sim {
 #endif
 
   // `lds` = this wave's LDS block: [hot copy (if resident) | scratch]; resident=false keeps hot in HBM.
+  // row_cold: observe()'s stage -> row map in the cold block whatever the layout says (a kernel that gives the LDS the
+  // layout left for it to something else: the persistent Decima rollout's policy plan).
   __device__ __forceinline__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* lds,
-                                 uint8_t* obs_arena, int32_t env_index, bool resident)
+                                 uint8_t* obs_arena, int32_t env_index, bool resident, bool row_cold = false)
       : L(p->L), D(p->D), C(p->C), IV(p->iv), NE(kN ? kN : p->L.num_executors), JC(kJ ? kJ : p->L.job_cap),
         SC(kS ? kS : p->L.stage_cap), O(kWin ? window_offsets(NE, kWJ, kWS) : state_offsets(NE, JC, SC)),
         OH(state_offsets(NE, JC, SC)),
@@ -327,7 +329,7 @@ struct Sim {
         hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * OH.env_bytes),
         cold(state_arena + kParamsReserve + (int64_t)env_index * OH.env_bytes + OH.hot_bytes),
         scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index), res(resident),
-        row_lds(kWin || resident || W::uni(p->O.row_of_lds) != 0) {
+        row_lds(kWin || resident || (!row_cold && W::uni(p->O.row_of_lds) != 0)) {
     iv_lane = W::lane() < kIvRows ? *reinterpret_cast<const uint32_t*>(IV[W::lane()]) : 0u;
     dcache_on = kDurCache && W::uni(p->hp.dcache) != 0;
     HPp = &p->hp;

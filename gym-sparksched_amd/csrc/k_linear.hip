@@ -4,12 +4,12 @@
 // per minibatch over 1e5..3e5 node rows with 5..64 features. Through hipBLASLt each call cost ~70 us of host time
 // (per-shape heuristics for row counts that change every minibatch) and its tall-skinny weight gradients ran on a
 // handful of workgroups (0.38 s of the learner's 0.71 s of GPU time, profiles/r04/learner_profile.log). Here:
-//   * ssim_linear_fwd: y[r][j] = b[j] + sum_i x[r][i] w(i, j) with the <= 64 x 64 weight staged in LDS, four outputs
-//     per thread (the forward: w(i, j) = W[j][i]; the input gradient: w(i, j) = W[i][j], no bias);
-//   * ssim_linear_wgrad: gW[j][i] = sum_r gy[r][j] x[r][i] and gb[j] = sum_r gy[r][j], split over 256-row chunks into
-//     per-chunk partial sums (LDS-staged row tiles, 4 x 4 output tiles per thread), then
-//     reduced in chunk order: deterministic, no atomics.
-// f32 in, f32 fma accumulation in index order; the learner's tolerance tests compare with torch (tests/test_linear_gpu).
+//   * ssim_linear_fwd: y[r][j] = b[j] + sum_i x[r][i] w(i, j) on the matrix cores (16-row tiles per wave, the <= 64 x 64
+//     weight staged in LDS in operand order; the forward: w(i, j) = W[j][i]; the input gradient: w(i, j) = W[i][j]);
+//   * ssim_linear_wgrad: gW[j][i] = sum_r gy[r][j] x[r][i] and gb[j] = sum_r gy[r][j] on the matrix cores, split over
+//     256-row chunks into per-chunk partial sums (LDS-staged row tiles), then reduced in chunk order: deterministic.
+// f32 operands, f32 accumulation (v_mfma_f32_16x16x4_f32: no reduced precision); the learner's tolerance tests compare
+// with torch (tests/test_linear_gpu). (Round 4's scalar forms read each row's inputs with stride in_dim per lane.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -19,110 +19,127 @@ namespace {
 
 constexpr int kLinMax = 64;   // widest layer
 constexpr int kFwdThreads = 256;
+constexpr int kFwdWaves = kFwdThreads / 64;
 constexpr int kWgThreads = 256;
 constexpr int kWgRows = 256;  // rows per chunk of the weight-gradient pass (one partial per chunk)
 constexpr int kWgTile = 64;   // rows per LDS tile within a chunk
+constexpr int kXs = 68;       // LDS row stride (floats) of the staged row tiles: 64 + 4 (16-B aligned, bank-skewed)
+constexpr int kXs2 = 80;      // ... of [x | 1] in the weight-gradient pass (in_dim + 1 <= 65 columns)
 
-// y[r][j..j+3] per thread (4 outputs of one row: the row's inputs are read once per 4 outputs, the weights as one
-// 16-B LDS read per input)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// y[r][j] = b[j] + sum_i x[r][i] w(i, j) on the matrix cores (v_mfma_f32_16x16x4_f32: f32 operands, f32 accumulate).
+// Each wave computes 16-row tiles: Y^T[16 units x 16 rows] = W^T . X^T per 16-unit output tile, the k order of the
+// steps being 16g + 4q + r (lane quarter q, word r), so one 16-B LDS word per lane gives four steps of each operand.
+// The weights are staged once per workgroup in that operand order (wp), each row tile is staged coalesced (the tile's
+// 16 x in_dim floats are contiguous in x) into the wave's LDS rows (stride kXs, zero-padded to the 16-k groups).
 __global__ __launch_bounds__(kFwdThreads) void k_linear_fwd(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ b, float* __restrict__ y,
                                                            int64_t rows, int in_dim, int out_dim, int transpose_w) {
-  __shared__ float4 m[kLinMax * (kLinMax / 4)];  // m[i][q] = w(i, 4q .. 4q + 3), zero past out_dim
-  const int nq = (out_dim + 3) / 4;
-  for (int t = threadIdx.x; t < in_dim * nq * 4; t += kFwdThreads) {
-    const int i = t / (nq * 4), j = t - i * nq * 4;
-    const float v = j >= out_dim ? 0.0f : transpose_w ? w[(int64_t)j * in_dim + i] : w[(int64_t)i * out_dim + j];
-    reinterpret_cast<float*>(m)[t] = v;
+  __shared__ f32x4 wp[4][4][64];  // [out tile t][k group g][lane]: word r = w(16g + 4(l >> 4) + r, 16t + (l & 15))
+  __shared__ __attribute__((aligned(16))) float bs[kLinMax];
+  __shared__ __attribute__((aligned(16))) float xs[kFwdWaves][16][kXs];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 4 * 4 * 64 * 4; e += kFwdThreads) {
+    const int r = e & 3, l = (e >> 2) & 63, g = (e >> 8) & 3, t = e >> 10;
+    const int j = 16 * t + (l & 15), i = 16 * g + 4 * (l >> 4) + r;
+    float v = 0.0f;
+    if (i < in_dim && j < out_dim) v = transpose_w ? w[(int64_t)j * in_dim + i] : w[(int64_t)i * out_dim + j];
+    reinterpret_cast<float*>(wp)[e] = v;
   }
+  for (int j = tid; j < kLinMax; j += kFwdThreads) bs[j] = (b != nullptr && j < out_dim) ? b[j] : 0.0f;
   __syncthreads();
-  const int64_t total = rows * nq;
-  for (int64_t g = (int64_t)blockIdx.x * kFwdThreads + threadIdx.x; g < total; g += (int64_t)gridDim.x * kFwdThreads) {
-    const int64_t r = g / nq;
-    const int q = (int)(g - r * nq), j0 = 4 * q;
-    const float* xr = x + r * in_dim;
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-    if (b != nullptr) {
-      a0 = b[j0];
-      if (j0 + 1 < out_dim) a1 = b[j0 + 1];
-      if (j0 + 2 < out_dim) a2 = b[j0 + 2];
-      if (j0 + 3 < out_dim) a3 = b[j0 + 3];
+  const int wave = tid >> 6, lane = tid & 63, row = lane & 15, q = lane >> 4;
+  const int KG = (in_dim + 15) / 16, NT = (out_dim + 15) / 16, kpad = 16 * KG;
+  float* xw = &xs[wave][0][0];
+  const int64_t tiles = (rows + 15) / 16;
+  for (int64_t tile = (int64_t)blockIdx.x * kFwdWaves + wave; tile < tiles; tile += (int64_t)gridDim.x * kFwdWaves) {
+    const int64_t r0 = tile * 16;
+    const int nr = rows - r0 < 16 ? (int)(rows - r0) : 16;
+    const float* xt = x + r0 * in_dim;
+#pragma unroll 4
+    for (int rr = 0; rr < 16; ++rr)
+      for (int k = lane; k < kpad; k += 64) xw[rr * kXs + k] = (rr < nr && k < in_dim) ? xt[rr * in_dim + k] : 0.0f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = 0; t < NT; ++t) {
+      f32x4 acc = *reinterpret_cast<const f32x4*>(&bs[16 * t + 4 * q]);
+      for (int g = 0; g < KG; ++g) {
+        const f32x4 a = wp[t][g][lane];
+        const f32x4 v = *reinterpret_cast<const f32x4*>(&xw[row * kXs + 16 * g + 4 * q]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[r], v[r], acc, 0, 0, 0);
+      }
+      if (row < nr) {  // lane holds y[r0 + row][16t + 4q + r]
+        float* yr = y + (r0 + row) * out_dim;
+        const int j0 = 16 * t + 4 * q;
+        if ((out_dim & 3) == 0 && j0 + 3 < out_dim) {
+          *reinterpret_cast<f32x4*>(yr + j0) = acc;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (j0 + r < out_dim) yr[j0 + r] = acc[r];
+        }
+      }
     }
-    for (int i = 0; i < in_dim; ++i) {
-      const float xv = xr[i];
-      const float4 mv = m[i * nq + q];
-      a0 = __builtin_fmaf(xv, mv.x, a0);
-      a1 = __builtin_fmaf(xv, mv.y, a1);
-      a2 = __builtin_fmaf(xv, mv.z, a2);
-      a3 = __builtin_fmaf(xv, mv.w, a3);
-    }
-    float* yr = y + r * out_dim + j0;
-    yr[0] = a0;
-    if (j0 + 1 < out_dim) yr[1] = a1;
-    if (j0 + 2 < out_dim) yr[2] = a2;
-    if (j0 + 3 < out_dim) yr[3] = a3;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the next tile overwrites the wave's rows)
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-// partial[p][j * (in_dim + 1) + i] over the rows of chunk p (kWgRows): i < in_dim the weight gradient, i == in_dim
-// the bias gradient (an input column of ones). Each thread owns 4 x 4 output tiles (rows j, columns i) and per row
-// reads 4 gradients and 4 inputs (two 16-B LDS reads) for 16 fmas.
+// partial[p][j * (in_dim + 1) + i] over the rows of chunk p (kWgRows): i < in_dim the weight gradient, i == in_dim the
+// bias gradient (an input column of ones), on the matrix cores: D[16 j x 16 i] += gY^T[j][4 rows] . X[4 rows][i] per
+// step, over the chunk's rows in order (deterministic). The chunk's rows are staged in 64-row LDS tiles (gy and
+// [x | 1], coalesced); the <= 4 x 5 output tiles are spread over the 4 waves.
 __global__ __launch_bounds__(kWgThreads) void k_linear_wgrad_part(const float* __restrict__ gy,
                                                                  const float* __restrict__ x, float* __restrict__ part,
                                                                  int64_t rows, int in_dim, int out_dim) {
-  __shared__ float4 gs[kWgTile * (kLinMax / 4)];
-  __shared__ float4 xs[kWgTile * ((kLinMax + 4) / 4)];
+  __shared__ __attribute__((aligned(16))) float gs[kWgTile][kXs];
+  __shared__ __attribute__((aligned(16))) float xs2[kWgTile][kXs2];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 15, q = lane >> 4;
   const int w1 = in_dim + 1, n_out = out_dim * w1;
-  const int tj = (out_dim + 3) / 4, ti = (w1 + 3) / 4, n_tiles = tj * ti;
+  const int IT = (w1 + 15) / 16, tiles = ((out_dim + 15) / 16) * IT;
   const int64_t r0 = (int64_t)blockIdx.x * kWgRows;
   const int64_t r1 = r0 + kWgRows < rows ? r0 + kWgRows : rows;
-  // up to 2 tiles per thread (64 x 65 outputs: 16 x 17 = 272 tiles on 256 threads)
-  float acc[2][16];
+  f32x4 acc[5];  // this wave's output tiles wave, wave + 4, ... (<= 5 of the <= 20)
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) acc[u][v] = 0.0f;
+  for (int u = 0; u < 5; ++u) acc[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   for (int64_t t0 = r0; t0 < r1; t0 += kWgTile) {
     const int nt = (int)(r1 - t0 < kWgTile ? r1 - t0 : kWgTile);
     __syncthreads();
-    for (int t = threadIdx.x; t < nt * tj * 4; t += kWgThreads) {
-      const int rr = t / (tj * 4), j = t - rr * tj * 4;
-      reinterpret_cast<float*>(gs)[t] = j < out_dim ? gy[(t0 + rr) * out_dim + j] : 0.0f;
+    for (int e = tid; e < kWgTile * 64; e += kWgThreads) {
+      const int rr = e >> 6, j = e & 63;
+      gs[rr][j] = (rr < nt && j < out_dim) ? gy[(t0 + rr) * out_dim + j] : 0.0f;
     }
-    for (int t = threadIdx.x; t < nt * ti * 4; t += kWgThreads) {
-      const int rr = t / (ti * 4), i = t - rr * ti * 4;
-      reinterpret_cast<float*>(xs)[t] = i < in_dim ? x[(t0 + rr) * in_dim + i] : i == in_dim ? 1.0f : 0.0f;
+    for (int e = tid; e < kWgTile * kXs2; e += kWgThreads) {
+      const int rr = e / kXs2, i = e - rr * kXs2;
+      xs2[rr][i] = rr >= nt ? 0.0f : i < in_dim ? x[(t0 + rr) * in_dim + i] : i == in_dim ? 1.0f : 0.0f;
     }
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int tile = threadIdx.x + u * kWgThreads;
-      if (tile < n_tiles) {
-        const int a = tile / ti, c = tile - a * ti;
-        for (int rr = 0; rr < nt; ++rr) {
-          const float4 g4 = gs[rr * tj + a];
-          const float4 x4 = xs[rr * ti + c];
-          const float gv[4] = {g4.x, g4.y, g4.z, g4.w}, xv[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-          for (int p = 0; p < 4; ++p)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[u][4 * p + q] = __builtin_fmaf(gv[p], xv[q], acc[u][4 * p + q]);
-        }
+    for (int u = 0; u < 5; ++u) {
+      const int tile = wave + 4 * u;
+      if (tile < tiles) {
+        const int tj = tile / IT, ti = tile - tj * IT;
+        const int j = 16 * tj + li, i = 16 * ti + li;
+#pragma unroll 4
+        for (int s = 0; s < kWgTile / 4; ++s)
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(gs[4 * s + q][j], xs2[4 * s + q][i], acc[u], 0, 0, 0);
       }
     }
   }
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int tile = threadIdx.x + u * kWgThreads;
-    if (tile < n_tiles) {
-      const int a = tile / ti, c = tile - a * ti;
+  for (int u = 0; u < 5; ++u) {
+    const int tile = wave + 4 * u;
+    if (tile < tiles) {
+      const int tj = tile / IT, ti = tile - tj * IT;
+      const int i = 16 * ti + li;
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int j = 4 * a + p, i = 4 * c + q;
-          if (j < out_dim && i < w1) part[(int64_t)blockIdx.x * n_out + j * w1 + i] = acc[u][4 * p + q];
-        }
+      for (int r = 0; r < 4; ++r) {  // lane holds D[4q + r][li] = gW[16 tj + 4q + r][16 ti + li]
+        const int j = 16 * tj + 4 * q + r;
+        if (j < out_dim && i < w1) part[(int64_t)blockIdx.x * n_out + j * w1 + i] = acc[u][r];
+      }
     }
   }
 }
@@ -166,9 +183,9 @@ int ssim_linear_fwd(const float* x, const float* w, const float* b, float* y, in
                     int32_t out_dim, int32_t transpose_w, void* stream) {
   if (!dims_ok(in_dim, out_dim) || rows < 0) return -1;
   if (rows == 0) return 0;
-  const int64_t total = rows * ((out_dim + 3) / 4);
-  int64_t blocks = (total + kFwdThreads - 1) / kFwdThreads;  // (total: rows x output quads)
-  if (blocks > 8192) blocks = 8192;  // grid-stride beyond: 32 workgroups per CU
+  const int64_t tiles = (rows + 15) / 16;  // 16-row tiles, one per wave at a time
+  int64_t blocks = (tiles + kFwdWaves - 1) / kFwdWaves;
+  if (blocks > 2048) blocks = 2048;  // grid-stride beyond: 8 workgroups per CU
   hipLaunchKernelGGL(k_linear_fwd, dim3((unsigned)blocks), dim3(kFwdThreads), 0, (hipStream_t)stream, x, w, b, y,
                      rows, (int)in_dim, (int)out_dim, (int)transpose_w);
   return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -107,12 +107,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
 // kWS / kWJ > 0 (with kRes): the windowed engine (engine.h) runs the env from an LDS copy of its live window; an env
 // whose window does not fit the rings, at the launch's start or later, continues on the HBM-resident engine in the
 // same wave (both engines are inlined; the HBM path is the rare one).
+// row_cold: the engine keeps observe()'s row map in the cold block (Sim), leaving the layout's LDS for the row map to
+// the action driver (the Decima rollout's policy plan).
 template <bool kRes, int kN, int kJ, int kS, class Pol, int kWS = 0, int kWJ = 0>
 __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                 const Pol& pol, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
                                                 int32_t* action_log, uint64_t* prof_out, int64_t budget,
-                                                const int32_t* __restrict__ env_steps) {
+                                                const int32_t* __restrict__ env_steps, bool row_cold = false) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
   if (budget > 0 && eid == 0 && WaveHip::lane() <= kStopLines)  // the next budget launch's slot (TicketStop)
@@ -182,7 +184,7 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
 #ifdef SSIM_PROFILE
   const uint64_t rt_entry = WaveHip::realtime();
 #endif
-  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kResHere);
+  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kResHere, row_cold);
 #ifdef SSIM_PROFILE
   s.prof_set(kTCtor, WaveHip::realtime());
 #endif

@@ -62,13 +62,22 @@ __global__ __launch_bounds__(64) void k_decima(const Params* __restrict__ P, con
   v.run(nts, ws, g_smem, feats, ccap, emask, depth);
 }
 
+// The policy parameters (DecimaScheduler.parameters() order, nn.Linear layout) into the matrix cores' packed layout
+// (decima_policy.h Mlp3P); one thread per packed float.
+__global__ __launch_bounds__(256) void k_decima_pack(const float* __restrict__ params, float* __restrict__ packed) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= 4 * kDpPacked) return;
+  const int src = dp_pack_src(f);
+  packed[f] = src >= 0 ? params[src] : 0.0f;
+}
+
 // `plan` null: the plan in LDS (dynamic shared memory); else a per-env region of global memory (stride plan_stride),
 // for node caps whose plan exceeds the LDS of a workgroup.
 template <bool kGlobal>
 __global__ __launch_bounds__(64) void k_decima_policy(const Params* __restrict__ P, const uint8_t* __restrict__ obs,
                                                       const float* __restrict__ feats, const int32_t* __restrict__ ccap,
                                                       const uint32_t* __restrict__ emask,
-                                                      const int32_t* __restrict__ depth, const float* __restrict__ Wt,
+                                                      const int32_t* __restrict__ depth, const dp_f32x4* __restrict__ Wt,
                                                       int node_cap, uint64_t seed, uint64_t counter,
                                                       const uint8_t* __restrict__ env_mask, DecimaPolicyOut o,
                                                       int32_t* overflow, uint8_t* plan, int64_t plan_stride) {
@@ -84,7 +93,8 @@ __global__ __launch_bounds__(64) void k_decima_policy(const Params* __restrict__
     return;
   }
   uint8_t* lds = kGlobal ? plan + (int64_t)eid * plan_stride : g_smem;
-  if (!decima_policy_env<kGlobal>(P, obs, feats, ccap, emask, depth, Wt, node_cap, seed, counter, eid, lds, o) &&
+  if (!decima_policy_env<kGlobal>(P, obs, feats, ccap, emask, depth, DpWGlobal{Wt}, node_cap, seed, counter, eid, lds,
+                                  o) &&
       WaveHip::lane() == 0 && overflow != nullptr)
     atomicAdd(overflow, 1);
 }
@@ -177,6 +187,7 @@ struct ssim_handle {
   uint64_t* prof_next = nullptr;  // -DSSIM_PROFILE builds: per-wave phase sums of the next Decima rollout launch
   uint8_t* policy_plan = nullptr;  // ssim_decima_policy's global plan when a node cap's plan exceeds the LDS
   int64_t policy_plan_bytes = 0;
+  void* policy_packed = nullptr;   // ssim_decima_policy's packed weights (kDpPackedBytes)
 };
 
 static thread_local char g_err[512] = "";
@@ -192,6 +203,12 @@ static int set_err(int code, const char* fmt, ...) {
 static int hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) return set_err(SSIM_E_HIP, "%s: %s", what, hipGetErrorString(e));
   return SSIM_OK;
+}
+
+static int decima_pack(const float* params, void* packed, void* stream) {
+  hipLaunchKernelGGL(k_decima_pack, dim3((4 * kDpPacked + 255) / 256), dim3(256), 0, (hipStream_t)stream, params,
+                     static_cast<float*>(packed));
+  return hip_check(hipGetLastError(), "k_decima_pack launch");
 }
 
 // A launch with more than 64 KB of dynamic LDS (layout.h kLdsBudgetBig) needs the kernel's opt-in attribute. It is
@@ -313,6 +330,7 @@ extern "C" int ssim_create(const ssim_config* cfg, const ssim_dataset* dataset, 
 
 extern "C" int ssim_destroy(ssim_handle* h) {
   if (h != nullptr && h->policy_plan != nullptr) (void)hipFree(h->policy_plan);
+  if (h != nullptr && h->policy_packed != nullptr) (void)hipFree(h->policy_packed);
   delete h;
   return SSIM_OK;
 }
@@ -550,6 +568,15 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
   if (node_cap < (L.num_executors + kDpEmb - 1) / kDpEmb) node_cap = (L.num_executors + kDpEmb - 1) / kDpEmb;
   const int64_t lds = decima_policy_lds_bytes(node_cap, L.job_cap);
   DecimaPolicyOut o{stage_idx, num_exec, job_idx, exec_idx, lgprob, stage_scores, exec_scores};
+  if (h->policy_packed == nullptr) {
+    const int rc = hip_check(hipMalloc(&h->policy_packed, (size_t)kDpPackedBytes), "packed weights allocation");
+    if (rc != SSIM_OK) return rc;
+  }
+  {
+    const int rc = decima_pack(params, h->policy_packed, stream);
+    if (rc != SSIM_OK) return rc;
+  }
+  const dp_f32x4* wpk = static_cast<const dp_f32x4*>(h->policy_packed);
   if (lds > kDecimaPolicyLdsMax) {  // the plan in a handle-owned global region (grown on demand)
     const int64_t stride = (lds + 255) & ~int64_t(255), need = stride * L.num_envs;
     if (need > h->policy_plan_bytes) {
@@ -565,7 +592,7 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
       h->policy_plan_bytes = need;
     }
     hipLaunchKernelGGL(k_decima_policy<true>, dim3(L.num_envs), dim3(64), 0, (hipStream_t)stream, dparams(h), h->obs,
-                       node_feats, commit_cap, edge_mask, depth, params, node_cap, seed, counter, env_mask, o, overflow,
+                       node_feats, commit_cap, edge_mask, depth, wpk, node_cap, seed, counter, env_mask, o, overflow,
                        h->policy_plan, stride);
     return hip_check(hipGetLastError(), "k_decima_policy(global plan) launch");
   }
@@ -574,7 +601,7 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
     if (rc != SSIM_OK) return rc;
   }
   hipLaunchKernelGGL(k_decima_policy<false>, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream,
-                     dparams(h), h->obs, node_feats, commit_cap, edge_mask, depth, params, node_cap, seed, counter,
+                     dparams(h), h->obs, node_feats, commit_cap, edge_mask, depth, wpk, node_cap, seed, counter,
                      env_mask, o, overflow, (uint8_t*)nullptr, (int64_t)0);
   return hip_check(hipGetLastError(), "k_decima_policy launch");
 }
@@ -611,8 +638,12 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
     return set_err(SSIM_E_ARG, "ssim_decima_rollout: workspace of %lld B, needs %lld (ssim_decima_workspace_bytes)",
                    (long long)workspace_bytes, (long long)wl.total);
   DecimaRolloutArgs a{};
-  a.weights = params;
+  a.weights = reinterpret_cast<const dp_f32x4*>(static_cast<uint8_t*>(workspace) + wl.packed);
   a.work = static_cast<uint8_t*>(workspace);
+  {
+    const int rc = decima_pack(params, static_cast<uint8_t*>(workspace) + wl.packed, stream);
+    if (rc != SSIM_OK) return rc;
+  }
   a.wl = wl;
   a.num_tasks_scale = num_tasks_scale;
   a.work_scale = work_scale;
@@ -627,7 +658,32 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
   }
   const DecimaRolloutSet ks = pick_decima(h->params);
   const DecimaRolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
-  const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  if (ks.win_stages == 0) {  // the LDS plan: the CU's LDS share (decima_rollout.h)
+    const StateOffsets& O = h->params.O;
+    const int64_t eng = O.lds_resident ? O.hot_bytes + O.scratch_bytes : O.scratch_hbm_bytes;  // (HBM: row map cold)
+    const int64_t budget = O.lds_resident ? kLdsBudgetBig : kLdsPerCu / kHbmWorkgroupsPerCu;
+    // HBM-resident engines without the duration-descriptor cache hold only per-operation temporaries in their LDS
+    // scratch (set tables, key lists, the commitment plan), none live across a decision: the plan overlays them.
+#ifdef SSIM_PROFILE
+    const bool overlay = false;  // (the profile sums live in the scratch)
+#else
+    const bool overlay = !O.lds_resident && L.num_executors > kDurCacheMaxExecs;
+#endif
+    const int64_t off = overlay ? 0 : align16(O.lds_resident ? O.scratch_bytes : O.scratch_hbm_bytes);
+    const int64_t base = O.lds_resident ? O.hot_bytes : 0;  // (the plan offset is relative to the scratch block)
+    const int64_t room = budget - base - off;
+    int cap = 0;
+    while (cap < L.stage_cap && decima_policy_lds_bytes(cap + 1, kDpLdsDags) <= room &&
+           decima_scratch_bytes(cap + 1) <= room)
+      ++cap;
+    a.plan_cap = cap;
+    a.plan_off = (int32_t)off;
+    if (cap > 0) {
+      const int64_t need = base + off + decima_policy_lds_bytes(cap, kDpLdsDags);
+      lds = need > align16(eng) ? need : align16(eng);
+    }
+  }
   const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   if (total_decisions > 0 && h->ticket_slot) flags |= kFlagTicketSlot;

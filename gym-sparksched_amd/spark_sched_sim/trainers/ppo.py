@@ -135,6 +135,7 @@ class PPO:
                 self.collector = DeviceRolloutCollector(self.engine, self.scheduler, seed=rseed,
                                                         row_offset=self.row_lo)
         self.gen = torch.Generator(device=self.device).manual_seed(rseed)  # learner's minibatch shuffling
+        self.perm_fn = None  # (tests) epoch -> permutation of the samples, instead of the generator's
         self.time_limit_rngs = None
         if self.mean_time_limit:
             # one StochasticTimeLimit per row, seeded like the reference wrapper (seed=42, reseeded by reset seed)
@@ -246,10 +247,13 @@ class PPO:
         cont = True
         self.scheduler.train()
         counts = learner_counts(obs)
-        for _ in range(self.num_epochs):
+        for epoch in range(self.num_epochs):
             if not cont:
                 break
-            perm = torch.randperm(n, device=advg.device, generator=self.gen)  # DataLoader(shuffle=True)
+            if self.perm_fn is not None:
+                perm = self.perm_fn(epoch).to(advg.device)
+            else:
+                perm = torch.randperm(n, device=advg.device, generator=self.gen)  # DataLoader(shuffle=True)
             groups = [perm[k: k + bs] for k in range(0, n, bs)]
             plans = minibatch_plans(obs, counts, groups)
             for idx, (sizes, plan) in zip(groups, plans):
