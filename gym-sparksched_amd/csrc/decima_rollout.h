@@ -288,7 +288,7 @@ struct DecimaPolicy {
 #define SSIM_DECIMA_ROLLOUT_WAVES 4
 #endif
 // kN / kJ: executor count and job cap as compile-time constants (0 = read from the layout), as kernels.h.
-template <bool kRes, int kN, int kJ, int kWS, int kWJ>
+template <bool kRes, int kN, int kJ>
 __device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                     DecimaRolloutArgs a, int num_steps, int flags,
                                                     const double* __restrict__ limits, uint8_t* reset,
@@ -296,25 +296,22 @@ __device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P
   a.autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   a.test_reject = (flags & SSIM_ROLLOUT_TEST_REJECT) != 0;
   const DecimaPolicy pol{P, obs, a};
-  rollout_body<kRes, kN, kJ, 0, DecimaPolicy, kWS, kWJ>(P, state, obs, pol, num_steps, flags, limits, reset, action_log,
-                                                       prof_out, budget, nullptr, !kRes && kWS == 0);
+  rollout_body<kRes, kN, kJ, 0, DecimaPolicy>(P, state, obs, pol, num_steps, flags, limits, reset, action_log, prof_out,
+                                              budget, nullptr, !kRes);
 }
-// kWS / kWJ > 0: the windowed engine (kernels.h rollout_body), with kRes
-#define SSIM_DR_WAVES(kRes, kWS) ((kWS) > 0 ? SSIM_WIN_WAVES : (kRes) ? 1 : SSIM_DECIMA_ROLLOUT_WAVES)
-template <bool kRes, int kN = 0, int kJ = 0, int kWS = 0, int kWJ = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_DR_WAVES(kRes, kWS)))) void k_decima_rollout(
+#define SSIM_DR_WAVES(kRes) ((kRes) ? 1 : SSIM_DECIMA_ROLLOUT_WAVES)
+template <bool kRes, int kN = 0, int kJ = 0>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_DR_WAVES(kRes)))) void k_decima_rollout(
     const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
     const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget, uint64_t* prof_out) {
-  decima_rollout_body<kRes, kN, kJ, kWS, kWJ>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget,
-                                              prof_out);
+  decima_rollout_body<kRes, kN, kJ>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
 }
 // launches that are not measured (SSIM_ROLLOUT_WARMUP), under their own symbol
-template <bool kRes, int kN = 0, int kJ = 0, int kWS = 0, int kWJ = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_DR_WAVES(kRes, kWS)))) void k_decima_rollout_warmup(
+template <bool kRes, int kN = 0, int kJ = 0>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_DR_WAVES(kRes)))) void k_decima_rollout_warmup(
     const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
     const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget, uint64_t* prof_out) {
-  decima_rollout_body<kRes, kN, kJ, kWS, kWJ>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget,
-                                              prof_out);
+  decima_rollout_body<kRes, kN, kJ>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
 }
 
 using DecimaRolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, DecimaRolloutArgs, int, int, const double*,
@@ -323,9 +320,7 @@ struct DecimaRolloutSet {
   DecimaRolloutFn rollout, rollout_warmup;
   SetTraceFn set_trace;  // the set KAT through this unit's engine instantiation (kernels.h k_set_trace)
   const char* name;      // the translation unit (ssim_debug_kernel_name)
-  int win_jobs = 0, win_stages = 0;  // windowed engine: ring sizes
 };
 DecimaRolloutSet decima_rollout_hbm();    // k_dr_hbm.hip
 DecimaRolloutSet decima_rollout_hbm50();  // k_dr_hbm50.hip: 50 executors / 200 jobs
-DecimaRolloutSet decima_rollout_win50();  // k_dr_win50.hip: 50 executors / 200 jobs, windowed engine
 DecimaRolloutSet decima_rollout_lds();    // k_dr_lds.hip

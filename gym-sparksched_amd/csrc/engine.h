@@ -123,7 +123,7 @@ struct NoStop {
   __device__ __forceinline__ uint64_t issue() const { return 0; }
   __device__ __forceinline__ bool hit(uint64_t) const { return false; }
 };
-enum : int32_t { kSimIdle = 0, kSimDecision = 1, kSimPreempted = 2, kSimOverflow = 3 };
+enum : int32_t { kSimIdle = 0, kSimDecision = 1, kSimPreempted = 2 };
 
 // The launch constants the event loop reads (dataset pointers, config scalars, obs-arena offsets), filled on the
 // host by fill_hot_params. On device each lane of one VGPR holds one dword (Sim::hpv) and a field read is a
@@ -240,27 +240,15 @@ inline void fill_hot_params(Params* p) {
 // kN / kJ / kS: executor count, job cap and stage cap as compile-time constants (0 = read from the layout at
 // run time). A fully specialised instantiation sees every section offset (hot block, scratch), loop bound
 // and table size as a constant, so LDS accesses use immediate offsets and no SGPRs hold offsets.
-// kWS / kWJ (> 0): WINDOWED residency (layout.h window_offsets). The LDS copy holds the fixed sections plus rings of
-// kWS stages (stage records, stage pools, the active-stage and schedulable lists, the observation's row map) and kWJ
-// jobs (job records and times, job pools) covering the env's live window — the stages from the lowest one still
-// referenced to the last arrived job's, the jobs from the lowest one still referenced to the next to arrive — instead
-// of the whole hot block, whose per-stage / per-job sections stay at their home offsets in HBM. A record's ring slot
-// is its index modulo the ring size (sidx / jidx / pidx). A J = 200 env's live window is a few dozen stages
-// (scripts/pool_stats.py), so the LDS copy shrinks from the whole ~150 KB hot block to ~18 KB and several envs share
-// a CU. A window that would outgrow its rings stops the wave's windowed loop at an event boundary (kSimOverflow);
-// the kernel then continues the env on the HBM-resident path (kernels.h rollout_body).
-template <class W, int kN = 0, int kJ = 0, int kS = 0, int kWS = 0, int kWJ = 0>
+template <class W, int kN = 0, int kJ = 0, int kS = 0>
 struct Sim {
   using WT = W;
-  static constexpr bool kWin = kWS > 0;
-  static_assert(!kWin || (kWJ > 0 && (kWS & (kWS - 1)) == 0 && (kWJ & (kWJ - 1)) == 0), "power-of-two rings");
   const ssim_layout& L;
   const ssim_dataset& D;
   const ssim_config& C;
   const uint8_t (*IV)[4];    // Params::iv
   const int32_t NE, JC, SC;  // executors, job cap, stage cap
-  const StateOffsets O;      // the working copy's layout (= OH, or the window's when kWin); also the scratch layout
-  const StateOffsets OH;     // re-derived from (NE, JC, SC): the home layout in HBM (same function as the host layout)
+  const StateOffsets O;      // re-derived from (NE, JC, SC): the layout (same function as the host layout); scratch too
   uint8_t* ghot;  // this env's hot block in HBM
   uint8_t* hot;   // working copy of the hot block (LDS when resident, else == ghot)
   uint8_t* cold;  // this env's cold block in HBM
@@ -323,13 +311,12 @@ struct Sim {
   __device__ __forceinline__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* lds,
                                  uint8_t* obs_arena, int32_t env_index, bool resident, bool row_cold = false)
       : L(p->L), D(p->D), C(p->C), IV(p->iv), NE(kN ? kN : p->L.num_executors), JC(kJ ? kJ : p->L.job_cap),
-        SC(kS ? kS : p->L.stage_cap), O(kWin ? window_offsets(NE, kWJ, kWS) : state_offsets(NE, JC, SC)),
-        OH(state_offsets(NE, JC, SC)),
-        ghot(state_arena + kParamsReserve + (int64_t)env_index * OH.env_bytes),
-        hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * OH.env_bytes),
-        cold(state_arena + kParamsReserve + (int64_t)env_index * OH.env_bytes + OH.hot_bytes),
+        SC(kS ? kS : p->L.stage_cap), O(state_offsets(NE, JC, SC)),
+        ghot(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
+        hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
+        cold(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes + O.hot_bytes),
         scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index), res(resident),
-        row_lds(kWin || resident || (!row_cold && W::uni(p->O.row_of_lds) != 0)) {
+        row_lds(resident || (!row_cold && W::uni(p->O.row_of_lds) != 0)) {
     iv_lane = W::lane() < kIvRows ? *reinterpret_cast<const uint32_t*>(IV[W::lane()]) : 0u;
     dcache_on = kDurCache && W::uni(p->hp.dcache) != 0;
     HPp = &p->hp;
@@ -403,44 +390,7 @@ struct Sim {
     }
     W::sync();
   }
-  // copy_spans with different source and destination offsets (the windowed residency's ring copies)
-  struct Span2 {
-    int64_t src, dst, n;  // byte offsets (source, destination), 16-B units
-  };
-  template <int kSpans>
-  __device__ __forceinline__ void copy_spans2(uint8_t* dst, const uint8_t* src, const Span2 (&sp)[kSpans]) {
-    W::sync();
-    int64_t end[kSpans];
-    int64_t total = 0;
-#pragma unroll
-    for (int r = 0; r < kSpans; ++r) end[r] = (total += sp[r].n);
-    for (int64_t i0 = 0; i0 < total; i0 += (int64_t)W::kWidth * kCopyBatch) {
-      u32x4 v[kCopyBatch];
-      int64_t so[kCopyBatch], dof[kCopyBatch];
-#pragma unroll
-      for (int u = 0; u < kCopyBatch; ++u) {
-        const int64_t i = i0 + (int64_t)u * W::kWidth + W::lane();
-        int64_t a = -1, b = -1;
-#pragma unroll
-        for (int r = kSpans - 1; r >= 0; --r)
-          if (i < end[r]) {
-            const int64_t q = (i - (end[r] - sp[r].n)) * 16;
-            a = sp[r].src + q;
-            b = sp[r].dst + q;
-          }
-        so[u] = i < total ? a : -1;
-        dof[u] = b;
-        if (so[u] >= 0) v[u] = *reinterpret_cast<const u32x4*>(src + so[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < kCopyBatch; ++u)
-        if (so[u] >= 0) *reinterpret_cast<u32x4*>(dst + dof[u]) = v[u];
-    }
-    W::sync();
-  }
   int32_t live_lo = 0;  // first stage of the live range (set by load_hot; 0 after an in-launch reset)
-  int32_t job_lo = 0;   // windowed residency: first job of the job window (jobs [job_lo, next arrival] in the ring)
-  bool win_full = false;  // windowed residency: the next event is an arrival the rings cannot hold (kSimOverflow)
   // End of the live stage range: the stages of every arrived job (hot block in place).
   __device__ __forceinline__ int live_hi() const {
     const int a = h.arrivals;
@@ -488,173 +438,6 @@ struct Sim {
     }
     const int hi = live_hi();
     return lo < hi ? lo : hi;
-  }
-  // ---- windowed residency (kWin): ring copies between the home layout (HBM) and the LDS image ----
-  // The ring spans of records [lo, hi) of `unit` 16-B units each: home section `home` (index = record), ring section
-  // `ring` (index = record mod `cap`): at most two pieces (a range wraps once).
-  __device__ __forceinline__ static void ring_spans(int64_t home, int64_t ring, int cap, int unit, int lo, int hi,
-                                                    Span2* a, Span2* b, bool to_home) {
-    const int n = hi > lo ? hi - lo : 0;
-    const int s0 = lo & (cap - 1);
-    const int n0 = n < cap - s0 ? n : cap - s0;
-    const int64_t h0 = home + 16 * (int64_t)unit * lo, r0 = ring + 16 * (int64_t)unit * s0;
-    const int64_t h1 = home + 16 * (int64_t)unit * (lo + n0), r1 = ring;
-    *a = to_home ? Span2{r0, h0, (int64_t)unit * n0} : Span2{h0, r0, (int64_t)unit * n0};
-    *b = to_home ? Span2{r1, h1, (int64_t)unit * (n - n0)} : Span2{h1, r1, (int64_t)unit * (n - n0)};
-  }
-  // Jobs [jlo, jhi) and stages [slo, shi) between home and the rings (records, times, pools), plus the lists.
-  __device__ __forceinline__ void win_copy(bool to_home, int jlo, int jhi, int slo, int shi, bool lists) {
-    Span2 sp[13];
-    ring_spans(OH.jobs, O.jobs, kWJ, 2, jlo, jhi, &sp[0], &sp[1], to_home);
-    ring_spans(OH.jtimes, O.jtimes, kWJ, 1, jlo, jhi, &sp[2], &sp[3], to_home);
-    ring_spans(OH.pools + 16, O.pools + 16, kWJ, 1, jlo, jhi, &sp[4], &sp[5], to_home);
-    ring_spans(OH.stages, O.stages, kWS, 1, slo, shi, &sp[6], &sp[7], to_home);
-    ring_spans(OH.pools + 16 * (1 + (int64_t)JC), O.pools + 16 * (1 + (int64_t)kWJ), kWS, 1, slo, shi, &sp[8], &sp[9],
-               to_home);
-    const int64_t la = lists ? (2 * (int64_t)h.n_active_jobs + 15) >> 4 : 0;
-    const int64_t ls = lists ? (2 * (int64_t)h.n_active_stages + 15) >> 4 : 0;
-    const int64_t lq = lists ? (2 * (int64_t)h.n_sched + 15) >> 4 : 0;
-    sp[10] = to_home ? Span2{O.active_jobs, OH.active_jobs, la} : Span2{OH.active_jobs, O.active_jobs, la};
-    sp[11] = to_home ? Span2{O.active_stages, OH.active_stages, ls} : Span2{OH.active_stages, O.active_stages, ls};
-    sp[12] = to_home ? Span2{O.sched_list, OH.sched_list, lq} : Span2{OH.sched_list, O.sched_list, lq};
-    if (to_home)
-      copy_spans2(ghot, hot, sp);
-    else
-      copy_spans2(hot, ghot, sp);
-  }
-  // The fixed sections of the LDS image (header and accumulators; executors, selected list, commitments; the COMMON
-  // pool), which the home and window layouts hold at different offsets from the executors on.
-  __device__ __forceinline__ void win_fixed(bool to_home) {
-    const Span2 sp[3] = {{0, 0, O.jobs >> 4},
-                         to_home ? Span2{O.execs, OH.execs, (OH.stages - OH.execs) >> 4}
-                                 : Span2{OH.execs, O.execs, (OH.stages - OH.execs) >> 4},
-                         to_home ? Span2{O.pools, OH.pools, 1} : Span2{OH.pools, O.pools, 1}};
-    if (to_home)
-      copy_spans2(ghot, hot, sp);
-    else
-      copy_spans2(hot, ghot, sp);
-  }
-  // End of the job window: the jobs that arrived and the next one to arrive (its arrival time is read at every pop)
-  __device__ __forceinline__ int win_jhi() const { return h.arrivals < h.num_jobs ? h.arrivals + 1 : h.arrivals; }
-  // The lowest stage and job still referenced (scan_live_lo's rules; jobs also through the executors' jobs, job pools,
-  // the stage window's lowest stage and, for a step in progress, the jobs it has completed: its reward's union,
-  // jobtime). `home`: records read from the HBM home (before the rings hold them), else from the LDS image.
-  __device__ __forceinline__ void win_scan(bool home, int* slo_out, int* jlo_out) {
-    constexpr int kNone = 0x7FFFFFFF;
-    const int16_t* aj = home ? reinterpret_cast<const int16_t*>(ghot + OH.active_jobs) : H<int16_t>(O.active_jobs);
-    int slo = is_stage_pool(h.source) ? pool_stage(h.source) : kNone;
-    int jlo = (h.source > 0 && h.source <= JC) ? h.source - 1 : kNone;
-    for (int k0 = 0; k0 < h.n_active_jobs; k0 += W::kWidth) {
-      const int k = k0 + W::lane();
-      int b = kNone, jj = kNone;
-      if (k < h.n_active_jobs) {
-        jj = aj[k];
-        b = home ? reinterpret_cast<const JobRec*>(ghot + OH.jobs)[jj].base : job(jj).base;
-      }
-      slo = W::min_i(b < slo ? b : slo);
-      jlo = W::min_i(jj < jlo ? jj : jlo);
-    }
-    for (int k0 = 0; k0 < NE; k0 += W::kWidth) {  // (executor and commitment records: the LDS image's)
-      const int e = k0 + W::lane();
-      int b = kNone, jj = kNone;
-      if (e < NE) {
-        const ExecRec x = exr(e);
-        if (is_stage_pool(x.loc)) b = pool_stage(x.loc);
-        if (x.loc > 0 && x.loc <= JC) jj = x.loc - 1;
-        if (x.job >= 0 && x.job < jj) jj = x.job;
-        if (x.ev_seq >= 0 && x.ev_stage >= 0 && x.ev_stage < b) b = x.ev_stage;
-      }
-      slo = W::min_i(b < slo ? b : slo);
-      jlo = W::min_i(jj < jlo ? jj : jlo);
-    }
-    for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
-      const int k = k0 + W::lane();
-      int b = kNone, jj = kNone;
-      if (k < commit_cap_for(NE)) {
-        const CommitRec r = cm(k);
-        if (r.cnt > 0) {
-          if (is_stage_pool(r.src)) b = pool_stage(r.src);
-          if (is_stage_pool(r.dst) && pool_stage(r.dst) < b) b = pool_stage(r.dst);
-          if (r.src > 0 && r.src <= JC) jj = r.src - 1;
-          if (r.dst > 0 && r.dst <= JC && r.dst - 1 < jj) jj = r.dst - 1;
-        }
-      }
-      slo = W::min_i(b < slo ? b : slo);
-      jlo = W::min_i(jj < jlo ? jj : jlo);
-    }
-    // a step in progress (preempted, or stopped at the rings' limit) may have completed jobs its reward counts
-    if (pending() || !home) {
-      const int from = home ? 0 : job_lo;
-      for (int j0 = from; j0 < h.arrivals; j0 += W::kWidth) {
-        const int j = j0 + W::lane();
-        int jj = kNone;
-        if (j < h.arrivals) {
-          const JobRec r = home ? reinterpret_cast<const JobRec*>(ghot + OH.jobs)[j] : job(j);
-          if (r.state == kJobDone && r.done_dec == h.decisions) jj = j;
-        }
-        jlo = W::min_i(jj < jlo ? jj : jlo);
-      }
-    }
-    const int a = h.arrivals;
-    const JobRec* hj = reinterpret_cast<const JobRec*>(ghot + OH.jobs);
-    const int shi = a > 0 ? (home ? (int)W::uni(hj[a - 1].base) + (int)W::uni(hj[a - 1].nst) : live_hi()) : 0;
-    slo = slo < shi ? slo : shi;
-    if (slo < shi) {  // the job of the lowest stage (and so of every stage in the window) stays in the job window
-      const int js = home ? (int)W::uni(reinterpret_cast<const StageRec*>(ghot + OH.stages)[slo].job) : (int)st_job(slo);
-      jlo = js < jlo ? js : jlo;
-    }
-    jlo = jlo < a ? jlo : a;
-    *slo_out = slo;
-    *jlo_out = jlo;
-  }
-  // Windowed load: false if the env's live window does not fit the rings (the caller then runs it HBM-resident).
-  __device__ __forceinline__ bool load_window() {
-    win_fixed(false);
-    load_header();
-    win_full = false;
-    int slo, jlo;
-    win_scan(true, &slo, &jlo);
-    const JobRec* hj = reinterpret_cast<const JobRec*>(ghot + OH.jobs);
-    const int a = h.arrivals;
-    const int shi = a > 0 ? (int)W::uni(hj[a - 1].base) + (int)W::uni(hj[a - 1].nst) : 0;
-    const int jhi = win_jhi();
-    if (jhi - jlo > kWJ || shi - slo > kWS || h.n_active_stages > kWS || h.n_sched > kWS) return false;
-    job_lo = jlo;
-    live_lo = slo;
-    win_copy(false, jlo, jhi, slo, shi, true);
-    ev_regs_load();
-    return true;
-  }
-  __device__ __forceinline__ void save_window() {
-    win_fixed(true);
-    win_copy(true, job_lo, win_jhi(), live_lo, live_hi(), true);
-  }
-  // Room in the rings for job j's arrival (its stages, and the next job's records); advances the window first
-  // (writing the records that leave it back home) when it would not fit.
-  __device__ __forceinline__ bool win_admit(int j) {
-    const int bj = job_base(j), nj = job_nst(j);
-    const int jn = j + 1 < h.num_jobs ? j + 2 : j + 1;
-    const auto fits = [&]() {
-      return jn - job_lo <= kWJ && bj + nj - live_lo <= kWS && h.n_active_stages + nj <= kWS;
-    };
-    if (fits()) return true;
-    int slo, jlo;
-    win_scan(false, &slo, &jlo);
-    slo = slo < bj ? slo : bj;  // (the arriving job's own stages start at bj)
-    jlo = jlo < j ? jlo : j;
-    if (slo > live_lo || jlo > job_lo) {
-      win_copy(true, job_lo, jlo > job_lo ? jlo : job_lo, live_lo, slo > live_lo ? slo : live_lo, false);
-      if (jlo > job_lo) job_lo = jlo;
-      if (slo > live_lo) live_lo = slo;
-    }
-    return fits();
-  }
-  // The next job to arrive: its records into the job ring (windowed residency; the pop reads its arrival time).
-  __device__ __forceinline__ void win_fetch_job(int j) {
-    if (j >= h.num_jobs) return;
-    const Span2 sp[2] = {{OH.jobs + 32 * (int64_t)j, O.jobs + 32 * (int64_t)jidx(j), 2},
-                         {OH.jtimes + 16 * (int64_t)j, O.jtimes + 16 * (int64_t)jidx(j), 1}};
-    copy_spans2(hot, ghot, sp);
   }
   __device__ __forceinline__ void load_hot() {
     SSIM_TIC(t0);
@@ -780,20 +563,14 @@ struct Sim {
     return r;
   }
 
-  // records (layout.h); with windowed residency the per-stage / per-job records sit in ring slots (sidx / jidx / pidx)
-  __device__ __forceinline__ static int sidx(int g) { return kWin ? (g & (kWS - 1)) : g; }
-  __device__ __forceinline__ static int jidx(int j) { return kWin ? (j & (kWJ - 1)) : j; }
-  __device__ __forceinline__ int pidx(int p) const {  // pool code -> record slot (code 0 = COMMON)
-    if constexpr (!kWin) return p;
-    return p <= 0 ? p : p <= JC ? 1 + ((p - 1) & (kWJ - 1)) : 1 + kWJ + ((p - 1 - JC) & (kWS - 1));
-  }
-  __device__ __forceinline__ StageRec& stage(int g) const { return H<StageRec>(O.stages)[sidx(g)]; }
-  __device__ __forceinline__ JobRec& job(int j) const { return H<JobRec>(O.jobs)[jidx(j)]; }
-  __device__ __forceinline__ JobTimes& jtimes(int j) const { return H<JobTimes>(O.jtimes)[jidx(j)]; }
+  // records (layout.h)
+  __device__ __forceinline__ StageRec& stage(int g) const { return H<StageRec>(O.stages)[g]; }
+  __device__ __forceinline__ JobRec& job(int j) const { return H<JobRec>(O.jobs)[j]; }
+  __device__ __forceinline__ JobTimes& jtimes(int j) const { return H<JobTimes>(O.jtimes)[j]; }
   __device__ __forceinline__ ExecRec& exr(int e) const { return H<ExecRec>(O.execs)[e]; }
   __device__ __forceinline__ CommitRec& cm(int k) const { return H<CommitRec>(O.commits)[k]; }
-  __device__ __forceinline__ PoolRec& pool(int p) const { return H<PoolRec>(O.pools)[pidx(p)]; }
-  __device__ __forceinline__ double* recent() const { return reinterpret_cast<double*>(cold + OH.st_recent); }
+  __device__ __forceinline__ PoolRec& pool(int p) const { return H<PoolRec>(O.pools)[p]; }
+  __device__ __forceinline__ double* recent() const { return reinterpret_cast<double*>(cold + O.st_recent); }
   // stages (env-global index g = job base + local stage id); `done` is derived: rem + exe + done = tasks
   __device__ __forceinline__ UF<int16_t> st_job(int g) const { return {&stage(g).job}; }
   __device__ __forceinline__ UF<int16_t> st_ts(int g) const { return {&stage(g).ts}; }
@@ -838,7 +615,7 @@ struct Sim {
     return st_job(p - 1 - JC);
   }
   __device__ __forceinline__ PySetMeta* pmeta(int p) const { return reinterpret_cast<PySetMeta*>(&pool(p)); }
-  __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + OH.pool_tab + (int64_t)p * tab_stride_for(NE); }
+  __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + O.pool_tab + (int64_t)p * tab_stride_for(NE); }
   __device__ __forceinline__ UF<int16_t> cfrom(int p) const { return {&pool(p).cfrom}; }
   __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)W::uni(pool(p).used); }
 
@@ -2135,7 +1912,6 @@ struct Sim {
     h.n_active_jobs += 1;
     h.n_active_stages += n;
     if (pool_size(kPoolCommon) > 0) h.source = kPoolCommon;
-    if constexpr (kWin) win_fetch_job(j + 1);  // the next arrival's records (win_admit made room)
   }
 
   __device__ __forceinline__ void on_executor_arrival(int e, int g) {  // :440-450
@@ -2275,12 +2051,6 @@ struct Sim {
       const double ta = W::uni(ta_lane);
       const int sa = h.arrivals;  // arrivals were pushed first with seq 0..J-1
       if (be < 0 || ta < bt || (ta == bt && sa < bseq)) {
-        if constexpr (kWin) {
-          if (!win_admit(sa)) {  // the rings cannot take this arrival: stop before it (the state is between events)
-            win_full = true;
-            return false;
-          }
-        }
         *t = ta;
         *kind = kEvArrival;
         *e = -1;
@@ -2329,7 +2099,7 @@ struct Sim {
       const bool have = pop_event(&t, &kind, &e, &g, &seq);
       SSIM_MARK("pop_end");
       SSIM_TOC(t_pop, kPhPop);
-      if (!have) return (kWin && win_full) ? kSimOverflow : kSimIdle;
+      if (!have) return kSimIdle;
       SSIM_TIC(t_h);
       h.wall = t;
       h.events++;
@@ -2384,8 +2154,7 @@ struct Sim {
     if (span == 0.0) return 0.0;
     double part = 0.0;
     const double beta = HP(beta);
-    // (jobs below the job window completed in earlier decisions: never in this reward's union)
-    for (int j0 = kWin ? job_lo : 0; j0 < h.arrivals; j0 += W::kWidth) {
+    for (int j0 = 0; j0 < h.arrivals; j0 += W::kWidth) {
       const int j = j0 + W::lane();
       if (j < h.arrivals) {
         const JobRec jr = job(j);
@@ -2427,7 +2196,7 @@ struct Sim {
     const int src_job = source_job();
     const int16_t* act = H<int16_t>(O.active_stages);
     int16_t* sched = H<int16_t>(O.sched_list);
-    int16_t* row_of = row_lds ? S<int16_t>(O.sc_row_of) : reinterpret_cast<int16_t*>(cold + OH.row_of);
+    int16_t* row_of = row_lds ? S<int16_t>(O.sc_row_of) : reinterpret_cast<int16_t*>(cold + O.row_of);
     float* nodes = reinterpret_cast<float*>(obs + HP(ob_nodes)) + (int64_t)eid * SC * 3;
     uint8_t* front = obs + HP(ob_frontier) + (int64_t)eid * SC;
     int32_t* srank = reinterpret_cast<int32_t*>(obs + HP(ob_sched_rank)) + (int64_t)eid * SC;
@@ -2458,7 +2227,7 @@ struct Sim {
         obs_st(nodes + 3 * i + 2, s ? 1.0f : 0.0f);
         obs_st(front + i, (uint8_t)(sr.unmet == 0 ? 1 : 0));
         obs_st(srank + i, s ? r : -1);
-        row_of[sidx(g)] = (int16_t)i;
+        row_of[g] = (int16_t)i;
         if (s) {
           sched[r] = (int16_t)g;
           W::amin(&job(sr.job).pick, (sr.unmet == 0 ? 0 : 0x10000) | r);
@@ -2530,7 +2299,7 @@ struct Sim {
             const int c = base + __builtin_ctz(live);
             live &= live - 1;
             obs_st(links + 2 * o + 0, (int64_t)i);
-            obs_st(links + 2 * o + 1, (int64_t)row_of[sidx(c)]);
+            obs_st(links + 2 * o + 1, (int64_t)row_of[c]);
             o++;
           }
         } else {
@@ -2539,7 +2308,7 @@ struct Sim {
             const StageRec cr = stage(c);
             if (!(cr.rem == 0 && cr.exe == 0) && o < ecap) {
               obs_st(links + 2 * o + 0, (int64_t)i);
-              obs_st(links + 2 * o + 1, (int64_t)row_of[sidx(c)]);
+              obs_st(links + 2 * o + 1, (int64_t)row_of[c]);
               o++;
             }
           }
@@ -2620,7 +2389,7 @@ struct Sim {
   template <class Stop>
   __device__ __forceinline__ bool finish_step(double t0, const Stop& stop) {
     const int r = simulate(stop);
-    if ((Stop::kCan && r == kSimPreempted) || (kWin && r == kSimOverflow)) {
+    if (Stop::kCan && r == kSimPreempted) {
       W::sync();
       if (W::lane() == 0) {
         acc().pend_t0 = t0;

@@ -35,15 +35,6 @@ __device__ __forceinline__ bool env_idle(const Params* __restrict__ P, const uin
 #ifndef SSIM_HBM_STEP_WAVES
 #define SSIM_HBM_STEP_WAVES 4
 #endif
-// Waves per SIMD the windowed rollouts (kWS > 0) are compiled for: their LDS copy (~18 KB for a J = 200 env) lets
-// about two envs per SIMD share a CU, so they may use up to 256 VGPRs.
-#ifndef SSIM_WIN_WAVES
-#define SSIM_WIN_WAVES 2
-#endif
-// 1: a windowed rollout continues an env whose window outgrows the rings on the HBM-resident engine in the same wave
-#ifndef SSIM_WIN_FALLBACK
-#define SSIM_WIN_FALLBACK 1
-#endif
 constexpr int32_t kFlagTicketSlot = 0x100;  // internal k_rollout flag: use the second budget counter
 
 // The budget rollout's decision counter and "budget spent" flag. Claims take chunks of decisions from one atomic
@@ -104,12 +95,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
   s.save_hot();
 }
 
-// kWS / kWJ > 0 (with kRes): the windowed engine (engine.h) runs the env from an LDS copy of its live window; an env
-// whose window does not fit the rings, at the launch's start or later, continues on the HBM-resident engine in the
-// same wave (both engines are inlined; the HBM path is the rare one).
 // row_cold: the engine keeps observe()'s row map in the cold block (Sim), leaving the layout's LDS for the row map to
 // the action driver (the Decima rollout's policy plan).
-template <bool kRes, int kN, int kJ, int kS, class Pol, int kWS = 0, int kWJ = 0>
+template <bool kRes, int kN, int kJ, int kS, class Pol>
 __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                 const Pol& pol, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
@@ -141,50 +129,10 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
   RolloutCursor c{0, 0, 0};
   const double limit = limits != nullptr ? limits[eid] : __builtin_inf();
   uint8_t* rec = reset + (int64_t)eid * P->L.reset_stride;
-  if constexpr (kWS > 0) {
-    static_assert(kRes, "the windowed engine is LDS-resident");
-    Sim<WaveHip, kN, kJ, kS, kWS, kWJ> w(P, state, g_smem, obs, eid, true);
-    int why = kLoopReloadFailed;
-    if (w.load_window()) {
-      // an episode's reset runs on the home layout (HBM engine), then the window of the new episode is loaded
-      const auto reset_win = [&](Sim<WaveHip, kN, kJ, kS, kWS, kWJ>& x) {
-        x.save_window();
-        WaveHip::gsync();
-        {
-          Sim<WaveHip, kN, kJ, kS> r(P, state, g_smem, obs, eid, false);
-          r.load_header();
-          r.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limit, rec);
-        }
-        WaveHip::gsync();
-        return x.load_window();
-      };
-      why = rollout_loop(w, pol, stop, c, B, eid, num_steps, autoreset, action_log, reset_win);
-      if (why != kLoopReloadFailed) w.save_window();
-    }
-    if (why == kLoopDone) {
-      if (c.granted > 0) stop.give_back(c.granted);
-      return;
-    }
-    WaveHip::gsync();  // the window's home copy before the HBM engine reads it
-#if !SSIM_WIN_FALLBACK
-    {  // (experiment builds without the HBM engine: the env freezes with a capacity error instead)
-      Sim<WaveHip, kN, kJ, kS> x(P, state, g_smem, obs, eid, false);
-      x.load_header();
-      x.fail(SSIM_ERR_CAPACITY);
-      x.store_header();
-      x.write_err_only(0u);
-      if (c.granted > 0) stop.give_back(c.granted);
-      return;
-    }
-#endif
-  }
-  // HBM-resident (kRes false), LDS-resident with the whole hot block (kRes true, no window), or the windowed engine's
-  // fallback (kWS > 0: the hot block stays in HBM)
-  constexpr bool kResHere = kRes && kWS == 0;
 #ifdef SSIM_PROFILE
   const uint64_t rt_entry = WaveHip::realtime();
 #endif
-  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kResHere, row_cold);
+  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes, row_cold);
 #ifdef SSIM_PROFILE
   s.prof_set(kTCtor, WaveHip::realtime());
 #endif
@@ -195,7 +143,6 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
 #endif
   const auto reset_in_place = [&](Sim<WaveHip, kN, kJ, kS>& x) {
     x.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limit, rec);
-    return true;
   };
   rollout_loop(s, pol, stop, c, B, eid, num_steps, autoreset, action_log, reset_in_place);
   if (c.granted > 0) stop.give_back(c.granted);  // a chunk the wave could not use (its step cap or episode end)
@@ -217,18 +164,18 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
   const Params *__restrict__ P, uint8_t *state, uint8_t *obs, int kind, uint64_t seed, int num_steps, int flags, \
       const double *__restrict__ limits, uint8_t *reset, int32_t *action_log, uint64_t *prof_out, int64_t budget, \
       const int32_t *__restrict__ env_steps
-#define SSIM_ROLLOUT_WAVES(kRes, kWS) ((kWS) > 0 ? SSIM_WIN_WAVES : (kRes) ? 1 : SSIM_HBM_ROLLOUT_WAVES)
-template <bool kRes, int kN, int kJ, int kS, int kWS = 0, int kWJ = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_ROLLOUT_WAVES(kRes, kWS)))) void k_rollout(SSIM_ROLLOUT_ARGS) {
-  rollout_body<kRes, kN, kJ, kS, HeuristicPolicy, kWS, kWJ>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags,
-                                                            limits, reset, action_log, prof_out, budget, env_steps);
+#define SSIM_ROLLOUT_WAVES(kRes) ((kRes) ? 1 : SSIM_HBM_ROLLOUT_WAVES)
+template <bool kRes, int kN, int kJ, int kS>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_ROLLOUT_WAVES(kRes)))) void k_rollout(SSIM_ROLLOUT_ARGS) {
+  rollout_body<kRes, kN, kJ, kS, HeuristicPolicy>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags, limits,
+                                                  reset, action_log, prof_out, budget, env_steps);
 }
 // The same rollout under its own symbol for launches that are not measured (SSIM_ROLLOUT_WARMUP: a benchmark's
 // pre-roll and warm-up), so a profiler's per-kernel statistics of k_rollout cover the timed launches only.
-template <bool kRes, int kN, int kJ, int kS, int kWS = 0, int kWJ = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_ROLLOUT_WAVES(kRes, kWS)))) void k_rollout_warmup(SSIM_ROLLOUT_ARGS) {
-  rollout_body<kRes, kN, kJ, kS, HeuristicPolicy, kWS, kWJ>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags,
-                                                            limits, reset, action_log, prof_out, budget, env_steps);
+template <bool kRes, int kN, int kJ, int kS>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_ROLLOUT_WAVES(kRes)))) void k_rollout_warmup(SSIM_ROLLOUT_ARGS) {
+  rollout_body<kRes, kN, kJ, kS, HeuristicPolicy>(P, state, obs, HeuristicPolicy{kind, seed}, num_steps, flags, limits,
+                                                  reset, action_log, prof_out, budget, env_steps);
 }
 
 // Test hook (ssim_debug_set_trace_ex, tests/test_gpu_sets.py): a trace of CPython-set operations on one pool (job 0's)
@@ -282,22 +229,15 @@ struct KernelSet {
   RolloutFn rollout, rollout_warmup;
   SetTraceFn set_trace;  // the set KAT through this unit's engine instantiation (k_set_trace)
   const char* name;      // the translation unit (ssim_debug_kernel_name)
-  int win_jobs = 0, win_stages = 0;  // windowed rollouts: ring sizes (0: the rollout's residency is the layout's)
 };
 template <bool kRes, int kN, int kJ, int kS, int kTag>
 inline KernelSet kernel_set(const char* name) {
   return {k_step<kRes, kN, kJ, kS>, k_rollout<kRes, kN, kJ, kS>, k_rollout_warmup<kRes, kN, kJ, kS>,
           k_set_trace<WaveHip, kRes, kN, kJ, kS, kTag>, name};
 }
-// HBM-resident steps, windowed rollouts (rings of kWS stages / kWJ jobs; layout.h window_lds_bytes)
-template <int kN, int kJ, int kS, int kWS, int kWJ, int kTag>
-inline KernelSet kernel_set_windowed(const char* name) {
-  return {k_step<false, kN, kJ, kS>, k_rollout<true, kN, kJ, kS, kWS, kWJ>, k_rollout_warmup<true, kN, kJ, kS, kWS, kWJ>,
-          k_set_trace<WaveHip, false, kN, kJ, kS, kTag>, name, kWJ, kWS};
-}
 // Translation-unit tags of k_set_trace (one per k_*.hip)
-enum : int { kTagBench900 = 1, kTagBench, kTagLds, kTagHbm, kTagHbmN100, kTagHbmN10, kTagHbmN50, kTagWinN100, kTagWinN50,
-             kTagDrHbm, kTagDrHbm50, kTagDrLds, kTagDrWin50, kTagKatBad };
+enum : int { kTagBench900 = 1, kTagBench, kTagLds, kTagHbm, kTagHbmN100, kTagHbmN10, kTagHbmN50, kTagDrHbm, kTagDrHbm50,
+             kTagDrLds, kTagKatBad };
 SetTraceFn set_trace_kat_bad();  // k_hbm_n100.hip: the N = 100 / J = 200 instantiation on WaveHipKatBadPage
 // one per translation unit
 KernelSet kernels_bench900();  // k_bench900.hip: LDS-resident, 10 executors / 50 jobs / stage cap 900
@@ -307,5 +247,3 @@ KernelSet kernels_hbm();       // k_hbm.hip: hot block in HBM, any shape
 KernelSet kernels_hbm_n100();  // k_hbm_n100.hip: hot block in HBM, 100 executors / 200 jobs (configs[3] shard)
 KernelSet kernels_hbm_n10();   // k_hbm_n10.hip: hot block in HBM, 10 executors / 50 jobs (configs[1] env, large batches)
 KernelSet kernels_hbm_n50();   // k_hbm_n50.hip: hot block in HBM, 50 executors / 200 jobs (decima_tpch.yaml env)
-KernelSet kernels_win_n100();  // k_win_n100.hip: HBM-resident steps, windowed rollouts, 100 executors / 200 jobs
-KernelSet kernels_win_n50();   // k_win_n50.hip: HBM-resident steps, windowed rollouts, 50 executors / 200 jobs

@@ -250,22 +250,6 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   return O;
 }
 
-// The LDS image of WINDOWED residency (engine.h kWS / kWJ): the hot block's layout for a job cap of `wj` and a stage
-// cap of `ws` — the ring sizes — so its fixed sections line up with the home layout up to the job records and every
-// per-job / per-stage section holds one ring (pool records: COMMON, wj job pools, ws stage pools). Its scratch has a
-// ws-entry stage -> row map. (Its cold offsets are unused: the cold block stays at the home layout's.)
-constexpr StateOffsets window_offsets(int64_t N, int64_t wj, int64_t ws) { return state_offsets(N, wj, ws); }
-// Ring sizes of the windowed rollouts of the J = 200 shapes (configs[2] / [3]: live windows of tens of stages and a
-// handful of jobs, scripts/pool_stats.py; larger windows continue on the HBM-resident engine).
-constexpr int kWinStages = 128, kWinJobs = 32;
-// Dynamic LDS of a windowed rollout launch: the window image and its scratch, or the HBM-resident fallback's scratch
-// (which reuses the same LDS), whichever is larger.
-constexpr int64_t window_lds_bytes(int64_t N, int64_t J, int64_t S, int64_t wj, int64_t ws, bool row_of_lds) {
-  const StateOffsets W = window_offsets(N, wj, ws), H = state_offsets(N, J, S);
-  const int64_t win = W.hot_bytes + W.scratch_bytes, hbm = row_of_lds ? H.scratch_bytes : H.scratch_hbm_bytes;
-  return win > hbm ? win : hbm;
-}
-
 // Computes the public layout and the private offsets. Returns false on a bad / unsupported config. `chip_cus`: the
 // device's compute units (hipDeviceAttributeMultiprocessorCount; a partitioned device or another SKU has fewer), which
 // sets how many envs the LDS-resident kernels hold at once and so the batch size above which they run HBM-resident.

@@ -1,5 +1,5 @@
 // rollout.h — the decision loop of the fused rollouts (kernels.h rollout_body), independent of the wave policy W so
-// the test-only host build (tests/hostsim) runs the same loop, windowed residency and HBM fallback included.
+// the test-only host build (tests/hostsim) runs the same loop.
 #pragma once
 #include "engine.h"
 #include "policy.h"
@@ -39,20 +39,16 @@ struct HeuristicPolicy {  // fair / FIFO / random (policy.h)
   __device__ __forceinline__ void rejected(S&) const {}
 };
 
-// The state of one wave's rollout that outlives a switch from the windowed to the HBM-resident engine mid-launch.
+// The state of one wave's rollout within a launch.
 struct RolloutCursor {
   int k;             // decisions this launch started
   int64_t granted;   // budget decisions claimed and not yet started
   int64_t last;      // the budget counter at the wave's previous claim
 };
-enum : int32_t { kLoopDone = 0, kLoopToHbm = 1, kLoopReloadFailed = 2 };
-
 // The decision loop of a fused rollout on engine `s` (any residency). `reset_env(s)` resets a finished episode in
-// place (false: the windowed engine could not load the new episode's window, which the reset left at home:
-// kLoopReloadFailed); a step that outgrows the rings stops at an event boundary, pending (kSimOverflow), and the
-// loop returns kLoopToHbm with the window still to be written home. Either way the HBM path takes the env over.
+// place.
 template <class SimT, class Pol, class StopT, class ResetFn>
-__device__ __forceinline__ int rollout_loop(SimT& s, const Pol& pol, const StopT& stop, RolloutCursor& c, int B,
+__device__ __forceinline__ void rollout_loop(SimT& s, const Pol& pol, const StopT& stop, RolloutCursor& c, int B,
                                             int eid, int num_steps, bool autoreset, int32_t* action_log,
                                             const ResetFn& reset_env) {
   using W = typename SimT::WT;
@@ -73,12 +69,11 @@ __device__ __forceinline__ int rollout_loop(SimT& s, const Pol& pol, const StopT
 #ifdef SSIM_PROFILE
       const uint64_t tr = W::clock();
 #endif
-      const bool ok = reset_env(s);
+      reset_env(s);
 #ifdef SSIM_PROFILE
       s.prof_add(kPhReset, W::clock() - tr);
       s.prof_add(kCtReset, 1);
 #endif
-      if (!ok) return kLoopReloadFailed;
       continue;
     }
     double st0 = 0.0;
@@ -116,12 +111,7 @@ __device__ __forceinline__ int rollout_loop(SimT& s, const Pol& pol, const StopT
       if (!simulate) pol.done(s);
     }
     if (simulate) {
-      if (!s.finish_step(st0, stop)) {  // stopped mid-simulation: pending until the next launch / the HBM path
-        if constexpr (SimT::kWin) {
-          if (s.win_full) return kLoopToHbm;
-        }
-        break;
-      }
+      if (!s.finish_step(st0, stop)) break;  // stopped mid-simulation: pending until the next launch
       pol.done(s);
     }
 #ifdef SSIM_PROFILE
@@ -134,7 +124,6 @@ __device__ __forceinline__ int rollout_loop(SimT& s, const Pol& pol, const StopT
     }
 #endif
   }
-  return kLoopDone;
 }
 
 }  // namespace ssim

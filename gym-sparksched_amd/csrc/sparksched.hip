@@ -129,26 +129,9 @@ static bool generic_forced() {
   }();
   return on != 0;
 }
-#if SSIM_WITH_WINDOWED
-// Experiment builds with the windowed rollouts (k_win_*.hip, k_dr_win50.hip): SSIM_WINDOW=1 selects them for the
-// configs[2] / [3] shapes.
-static bool windowed_enabled() {
-  static const int on = [] {
-    const char* v = getenv("SSIM_WINDOW");
-    return (v != nullptr && v[0] == '1') ? 1 : 0;
-  }();
-  return on != 0;
-}
-#else
-static bool windowed_enabled() { return false; }
-#endif
 static KernelSet pick_kernels(const Params& p) {
   if (!p.O.lds_resident) {  // HBM-resident: the configs[2] / [3] shapes have (executors, jobs)-specialised kernels
     if (generic_forced()) return kernels_hbm();
-#if SSIM_WITH_WINDOWED
-    if (windowed_enabled() && large_shape(p)) return kernels_win_n100();
-    if (windowed_enabled() && decima_shape(p)) return kernels_win_n50();
-#endif
     if (large_shape(p)) return kernels_hbm_n100();
     if (decima_shape(p)) return kernels_hbm_n50();
     if (bench_shape(p)) return kernels_hbm_n10();
@@ -158,9 +141,6 @@ static KernelSet pick_kernels(const Params& p) {
   return kernels_lds();
 }
 static DecimaRolloutSet pick_decima(const Params& p) {
-#if SSIM_WITH_WINDOWED
-  if (!p.O.lds_resident && decima_shape(p) && windowed_enabled()) return decima_rollout_win50();
-#endif
   return p.O.lds_resident                          ? decima_rollout_lds()
          : !decima_shape(p) || generic_forced()   ? decima_rollout_hbm()
                                                   : decima_rollout_hbm50();
@@ -169,12 +149,6 @@ static StepFn pick_step(const Params& p) { return pick_kernels(p).step; }
 static RolloutFn pick_rollout(const Params& p, bool warmup = false) {
   const KernelSet k = pick_kernels(p);
   return warmup ? k.rollout_warmup : k.rollout;
-}
-// Dynamic LDS of a rollout launch: the layout's, or a windowed rollout's (window image + scratch, or the HBM
-// fallback's scratch)
-static int64_t rollout_lds(const Params& p, int win_jobs, int win_stages) {
-  if (win_stages == 0) return p.O.lds_bytes;
-  return window_lds_bytes(p.L.num_executors, p.L.job_cap, p.L.stage_cap, win_jobs, win_stages, p.O.row_of_lds != 0);
 }
 
 // ------------------------------------------------------------------------------------------ C ABI
@@ -382,7 +356,7 @@ static int rollout_launch(ssim_handle* h, int32_t kind, uint64_t seed, int32_t n
   const ssim_layout& L = h->params.L;
   const KernelSet ks = pick_kernels(h->params);
   const RolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
-  const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  const int64_t lds = h->params.O.lds_bytes;
   const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   // the budget slot this launch claims from; flipped only once the launch is enqueued (a failed launch leaves the
@@ -439,7 +413,7 @@ extern "C" int ssim_rollout_profiled(ssim_handle* h, int32_t kind, uint64_t seed
   const ssim_layout& L = h->params.L;
   const KernelSet ks = pick_kernels(h->params);
   const RolloutFn fn = ks.rollout;
-  const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  const int64_t lds = h->params.O.lds_bytes;
   const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream,
@@ -455,7 +429,7 @@ extern "C" int ssim_rollout_budget_profiled(ssim_handle* h, int32_t kind, uint64
   if (total_decisions <= 0) return set_err(SSIM_E_ARG, "ssim_rollout_budget_profiled: total_decisions must be > 0");
   const KernelSet ks = pick_kernels(h->params);
   const RolloutFn fn = ks.rollout;
-  const int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
+  const int64_t lds = h->params.O.lds_bytes;
   const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   if (h->ticket_slot) flags |= kFlagTicketSlot;
@@ -658,8 +632,8 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
   }
   const DecimaRolloutSet ks = pick_decima(h->params);
   const DecimaRolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
-  int64_t lds = rollout_lds(h->params, ks.win_jobs, ks.win_stages);
-  if (ks.win_stages == 0) {  // the LDS plan: the CU's LDS share (decima_rollout.h)
+  int64_t lds = h->params.O.lds_bytes;
+  {  // the LDS plan: the CU's LDS share (decima_rollout.h)
     const StateOffsets& O = h->params.O;
     const int64_t eng = O.lds_resident ? O.hot_bytes + O.scratch_bytes : O.scratch_hbm_bytes;  // (HBM: row map cold)
     const int64_t budget = O.lds_resident ? kLdsBudgetBig : kLdsPerCu / kHbmWorkgroupsPerCu;

@@ -26,7 +26,7 @@ for s in "$@"; do
     pytest)  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     pytestall) step pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread ;;
     pytestk) step pytest_k 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PYTEST_K" ;;
-    diag)    step diag_plain 240 env SSIM_WINDOW=0 python -u scripts/diag_large.py 64,20,0 4096,10,0 4096,5,8000 && step diag_win 240 python -u scripts/diag_large.py 64,20,0 4096,10,0 4096,5,8000 ;;
+    diag)    step diag_large 240 python -u scripts/diag_large.py 64,20,0 4096,10,0 4096,5,8000 ;;
     sets)    step pytest_sets 300 python -u -m pytest tests/test_gpu_sets.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
     bench_large_nocpu) step bench_large_nocpu 300 python bench.py --workload large --steps 100 --warmup 20 --no-cpu-baseline ;;
     bench_decima_nocpu) step bench_decima_nocpu 300 python bench.py --workload decima --steps 40 --warmup 5 --no-cpu-baseline ;;

@@ -35,7 +35,7 @@ def build_prof():
         return out  # prebuilt in-tree (build on the CPU container: `python scripts/phase_profile.py --build`)
     import __graft_entry__
 
-    return __graft_entry__.build_lib(force=True, out=out, defines=["-DSSIM_PROFILE"])
+    return __graft_entry__.build_lib(out=out, defines=["-DSSIM_PROFILE"])
 
 
 def main():

@@ -76,7 +76,6 @@ def lib():
         L.hs_reset_sampled.argtypes = [vp, vp, vp, vp]
         L.hs_rollout_ex.argtypes = [vp, ct.c_int, ct.c_uint64, ct.c_int, ct.c_int, vp, vp]
         L.hs_rollout_steps.argtypes = [vp, ct.c_int, ct.c_uint64, vp, ct.c_int, ct.c_int, vp, vp]
-        L.hs_rollout_windowed.argtypes = [vp, ct.c_int, ct.c_int, ct.c_uint64, ct.c_int, ct.c_int, vp, vp, vp]
         L.hs_seed_words.argtypes = [ct.c_uint64, vp]
         L.hs_std_exponential.argtypes = [vp, ct.c_int, vp]
         L.hs_log1p.argtypes = [vp, ct.c_int, vp]
@@ -158,18 +157,6 @@ class HostEngine:
                                  ptr)
         assert rc == 0, "hostsim rollout: the hot-block policy view disagreed with the obs-arena view" if rc == -5 \
             else f"hostsim rollout rc={rc}"
-
-    def rollout_windowed(self, kind, seed, num_steps, variant=0, action_log=None, flags=0, time_limits=None):
-        """The device's fused rollout on the windowed engine (hostsim.cpp rollout_windowed); returns the per-env
-        flags of envs that finished on the HBM-resident fallback."""
-        ptr = action_log.ctypes.data if action_log is not None else None
-        tl = None if time_limits is None else np.ascontiguousarray(np.asarray(time_limits, dtype=np.float64))
-        fb = np.zeros(self.num_envs, dtype=np.int32)
-        self._keep_tl = tl
-        rc = lib().hs_rollout_windowed(self.handle, variant, kind, seed, num_steps, flags,
-                                       None if tl is None else tl.ctypes.data, ptr, fb.ctypes.data)
-        assert rc == 0, f"hostsim rollout_windowed rc={rc}"
-        return fb
 
     def rollout_steps(self, kind, seed, env_steps, max_steps, action_log=None, flags=0, time_limits=None):
         st = np.ascontiguousarray(np.asarray(env_steps, dtype=np.int32).reshape(self.num_envs))

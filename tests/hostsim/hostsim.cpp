@@ -230,69 +230,6 @@ int hs_rollout_steps(hs_handle* h, int kind, uint64_t seed, const int32_t* env_s
   return 0;
 }
 
-// The device's fused rollout (kernels.h rollout_body) on the WINDOWED engine: per env the live window in a poisoned
-// LDS emulation (rings of WS stages / WJ jobs), auto-resets through the home layout, and the HBM-resident engine for
-// an env whose window outgrows the rings (at the start or mid-step, kSimOverflow). The same rollout_loop as the
-// device; no shared budget. fell_back[e]: 1 if env e finished the call on the HBM path.
-}  // extern "C"
-template <int WS, int WJ>
-static int rollout_windowed(hs_handle* h, int kind, uint64_t seed, int num_steps, int flags, const double* limits,
-                            int32_t* action_log, int32_t* fell_back) {
-  const Params* P = h->params;
-  const int B = P->L.num_envs;
-  const int64_t lds_bytes = window_lds_bytes(P->L.num_executors, P->L.job_cap, P->L.stage_cap, WJ, WS,
-                                             P->O.row_of_lds != 0);
-  uint8_t* lds = (uint8_t*)malloc((size_t)lds_bytes);
-  const HeuristicPolicy pol{kind, seed};
-  const NoBudget stop;
-  const bool autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
-  for (int e = 0; e < B; ++e) {
-    memset(lds, kPoison, (size_t)lds_bytes);
-    RolloutCursor c{0, 0, 0};
-    const double limit = limits ? limits[e] : __builtin_inf();
-    uint8_t* rec = h->reset + (int64_t)e * P->L.reset_stride;
-    fell_back[e] = 0;
-    Sim<WaveSerial, 0, 0, 0, WS, WJ> w(P, h->state, lds, h->obs, e, true);
-    if (w.load_window()) {
-      const auto reset_win = [&](Sim<WaveSerial, 0, 0, 0, WS, WJ>& s) {
-        s.save_window();
-        memset(lds, kPoison, (size_t)lds_bytes);
-        {
-          Sim<WaveSerial> r(P, h->state, lds, h->obs, e, false);
-          r.load_header();
-          r.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limit, rec);
-        }
-        memset(lds, kPoison, (size_t)lds_bytes);
-        return s.load_window();
-      };
-      const int why = rollout_loop(w, pol, stop, c, B, e, num_steps, autoreset, action_log, reset_win);
-      if (why != kLoopReloadFailed) w.save_window();
-      if (why == kLoopDone) continue;
-    }
-    fell_back[e] = 1;
-    memset(lds, kPoison, (size_t)lds_bytes);
-    Sim<WaveSerial> s(P, h->state, lds, h->obs, e, false);
-    s.load_hot();
-    const auto reset_in_place = [&](Sim<WaveSerial>& x) {
-      x.reset_sampled(SSIM_RESET_CONTINUE, 0ull, limit, rec);
-      return true;
-    };
-    rollout_loop(s, pol, stop, c, B, e, num_steps, autoreset, action_log, reset_in_place);
-    s.save_hot();
-  }
-  free(lds);
-  return 0;
-}
-extern "C" {
-
-// ring variant 0: the device's (kWinStages, kWinJobs); 1: tiny rings (overflows and falls back often)
-int hs_rollout_windowed(hs_handle* h, int variant, int kind, uint64_t seed, int num_steps, int flags,
-                        const double* limits, int32_t* action_log, int32_t* fell_back) {
-  if (variant == 0)
-    return rollout_windowed<kWinStages, kWinJobs>(h, kind, seed, num_steps, flags, limits, action_log, fell_back);
-  return rollout_windowed<32, 4>(h, kind, seed, num_steps, flags, limits, action_log, fell_back);
-}
-
 void hs_job_times(hs_handle* h, double* ta, double* tc, int32_t* st) {
   const Params* P = h->params;
   const int J = P->L.job_cap;

@@ -63,49 +63,3 @@ def test_autoreset_replay(make, dataset, env_cfg, mean_limit):
 
 def test_async_rollouts(make, dataset, env_cfg):
     cases.case_async_rollouts(make, dataset, env_cfg)
-
-
-WINDOW_CASES = [  # (config overrides, envs, steps, mean time limit, ring variant)
-    (dict(num_executors=100, job_arrival_cap=200), 3, 400, 2.0e5, 0),   # configs[3] shape, the device's rings
-    (dict(num_executors=50, job_arrival_cap=200), 3, 400, 2.0e5, 0),    # configs[2] env, the device's rings
-    (dict(num_executors=50, job_arrival_cap=200), 3, 300, 2.0e5, 1),    # tiny rings: overflow mid-step -> HBM path
-    (dict(), 4, 1500, None, 1),                                         # J = 50: windows outgrow tiny rings often
-]
-
-
-@pytest.mark.parametrize("cfg_over,B,K,mean_limit,variant", WINDOW_CASES)
-def test_windowed_rollout_matches_plain(dataset, env_cfg, cfg_over, B, K, mean_limit, variant):
-    """The device's fused rollout on the WINDOWED engine (rollout.h rollout_loop; engine.h kWS / kWJ: rings of stages
-    and jobs in a poisoned LDS emulation, auto-resets through the home layout, the HBM-resident engine for envs whose
-    window outgrows the rings) leaves every env exactly as the plain rollout does: the action log, every
-    observation field, the accumulators, wall times and job times. Variant 1's tiny rings (32 stages / 4 jobs) make
-    windows overflow at load, at arrivals mid-step and at reloads after resets, so the fallback paths run too."""
-    import numpy as np
-
-    from hostsim.driver import HostEngine
-    from spark_sched_sim.distributed import shard_seeds
-
-    cfg = dict(env_cfg, **cfg_over)
-    limits = cases.bench_time_limits(mean_limit, shard_seeds(0, B, 0)) if mean_limit else None
-    engs = [HostEngine(cfg, B, dataset) for _ in range(2)]
-    logs = []
-    for e in engs:
-        e.reset_sampled(_abi.SSIM_RESET_SEED, seeds=shard_seeds(0, B, 0), time_limits=limits)
-        logs.append(e.alloc_action_log(K))
-    flags = _abi.SSIM_ROLLOUT_AUTORESET
-    engs[0].rollout(_abi.SSIM_POLICY_RANDOM, 77, K, logs[0], flags=flags, time_limits=limits)
-    fell = engs[1].rollout_windowed(_abi.SSIM_POLICY_RANDOM, 77, K, variant=variant, action_log=logs[1], flags=flags,
-                                    time_limits=limits)
-    assert np.array_equal(logs[0], logs[1])
-    a, b = engs[0].host_views(), engs[1].host_views()
-    for k in a:
-        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
-    ta0, tc0, st0 = engs[0].job_times_np()
-    ta1, tc1, st1 = engs[1].job_times_np()
-    assert np.array_equal(ta0, ta1) and np.array_equal(tc0, tc1) and np.array_equal(st0, st1)
-    assert int(np.count_nonzero(a["counts"][:, _abi.OC_ERR])) == 0
-    assert int(a["acc"][:, _abi.ACC_EPISODES].sum()) > 0  # auto-resets ran inside the call
-    if variant == 1:
-        assert fell.any()  # the fallback path ran
-    else:
-        assert not fell.any()
