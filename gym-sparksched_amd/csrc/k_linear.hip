@@ -23,22 +23,22 @@ constexpr int kFwdWaves = kFwdThreads / 64;
 constexpr int kWgThreads = 256;
 constexpr int kWgRows = 256;  // rows per chunk of the weight-gradient pass (one partial per chunk)
 constexpr int kWgTile = 64;   // rows per LDS tile within a chunk
-constexpr int kXs = 68;       // LDS row stride (floats) of the staged row tiles: 64 + 4 (16-B aligned, bank-skewed)
+constexpr int kXs = 68;       // LDS row stride (floats) of the staged gy tiles: 64 + 4 (16-B aligned, bank-skewed)
 constexpr int kXs2 = 80;      // ... of [x | 1] in the weight-gradient pass (in_dim + 1 <= 65 columns)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // y[r][j] = b[j] + sum_i x[r][i] w(i, j) on the matrix cores (v_mfma_f32_16x16x4_f32: f32 operands, f32 accumulate).
 // Each wave computes 16-row tiles: Y^T[16 units x 16 rows] = W^T . X^T per 16-unit output tile, the k order of the
-// steps being 16g + 4q + r (lane quarter q, word r), so one 16-B LDS word per lane gives four steps of each operand.
-// The weights are staged once per workgroup in that operand order (wp), each row tile is staged coalesced (the tile's
-// 16 x in_dim floats are contiguous in x) into the wave's LDS rows (stride kXs, zero-padded to the 16-k groups).
+// steps being 16g + 4q + r (lane quarter q, word r): lane (row, q) loads its row's inputs 16g + 4q .. + 3 straight
+// into registers (the B operand of four steps), the weights are staged once per workgroup in the A operand's order
+// (wp: one 16-B LDS word per lane per four steps), and the <= 4 output tiles' accumulator chains are interleaved step
+// by step (independent MFMAs back to back instead of each waiting on its predecessor's result).
 __global__ __launch_bounds__(kFwdThreads) void k_linear_fwd(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ b, float* __restrict__ y,
                                                            int64_t rows, int in_dim, int out_dim, int transpose_w) {
   __shared__ f32x4 wp[4][4][64];  // [out tile t][k group g][lane]: word r = w(16g + 4(l >> 4) + r, 16t + (l & 15))
   __shared__ __attribute__((aligned(16))) float bs[kLinMax];
-  __shared__ __attribute__((aligned(16))) float xs[kFwdWaves][16][kXs];
   const int tid = threadIdx.x;
   for (int e = tid; e < 4 * 4 * 64 * 4; e += kFwdThreads) {
     const int r = e & 3, l = (e >> 2) & 63, g = (e >> 8) & 3, t = e >> 10;
@@ -50,41 +50,50 @@ __global__ __launch_bounds__(kFwdThreads) void k_linear_fwd(const float* __restr
   for (int j = tid; j < kLinMax; j += kFwdThreads) bs[j] = (b != nullptr && j < out_dim) ? b[j] : 0.0f;
   __syncthreads();
   const int wave = tid >> 6, lane = tid & 63, row = lane & 15, q = lane >> 4;
-  const int KG = (in_dim + 15) / 16, NT = (out_dim + 15) / 16, kpad = 16 * KG;
-  float* xw = &xs[wave][0][0];
+  const int KG = (in_dim + 15) / 16, NT = (out_dim + 15) / 16;
   const int64_t tiles = (rows + 15) / 16;
   for (int64_t tile = (int64_t)blockIdx.x * kFwdWaves + wave; tile < tiles; tile += (int64_t)gridDim.x * kFwdWaves) {
     const int64_t r0 = tile * 16;
-    const int nr = rows - r0 < 16 ? (int)(rows - r0) : 16;
-    const float* xt = x + r0 * in_dim;
-#pragma unroll 4
-    for (int rr = 0; rr < 16; ++rr)
-      for (int k = lane; k < kpad; k += 64) xw[rr * kXs + k] = (rr < nr && k < in_dim) ? xt[rr * in_dim + k] : 0.0f;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int t = 0; t < NT; ++t) {
-      f32x4 acc = *reinterpret_cast<const f32x4*>(&bs[16 * t + 4 * q]);
-      for (int g = 0; g < KG; ++g) {
-        const f32x4 a = wp[t][g][lane];
-        const f32x4 v = *reinterpret_cast<const f32x4*>(&xw[row * kXs + 16 * g + 4 * q]);
+    const bool valid = r0 + row < rows;
+    const float* xr = x + (r0 + row) * in_dim;
+    f32x4 xv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[r], v[r], acc, 0, 0, 0);
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 16 * g + 4 * q + j;
+        xv[g][j] = (g < KG && valid && k < in_dim) ? xr[k] : 0.0f;
       }
-      if (row < nr) {  // lane holds y[r0 + row][16t + 4q + r]
-        float* yr = y + (r0 + row) * out_dim;
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = *reinterpret_cast<const f32x4*>(&bs[16 * t + 4 * q]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (g >= KG) break;
+      f32x4 a[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[t] = wp[t][g][lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (t < NT) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][r], xv[g][r], acc[t], 0, 0, 0);
+    }
+    if (valid) {  // lane holds y[r0 + row][16t + 4q + r]
+      float* yr = y + (r0 + row) * out_dim;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
         const int j0 = 16 * t + 4 * q;
+        if (t >= NT) break;
         if ((out_dim & 3) == 0 && j0 + 3 < out_dim) {
-          *reinterpret_cast<f32x4*>(yr + j0) = acc;
+          *reinterpret_cast<f32x4*>(yr + j0) = acc[t];
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (j0 + r < out_dim) yr[j0 + r] = acc[r];
+            if (j0 + r < out_dim) yr[j0 + r] = acc[t][r];
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the next tile overwrites the wave's rows)
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -103,8 +112,14 @@ __global__ __launch_bounds__(kWgThreads) void k_linear_wgrad_part(const float* _
   const int64_t r0 = (int64_t)blockIdx.x * kWgRows;
   const int64_t r1 = r0 + kWgRows < rows ? r0 + kWgRows : rows;
   f32x4 acc[5];  // this wave's output tiles wave, wave + 4, ... (<= 5 of the <= 20)
+  int tj_j[5], ti_i[5];  // their operand columns: gy column 16 tj + li, [x | 1] column 16 ti + li
 #pragma unroll
-  for (int u = 0; u < 5; ++u) acc[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  for (int u = 0; u < 5; ++u) {
+    acc[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int tile = wave + 4 * u, tj = tile / IT, ti = tile - tj * IT;
+    tj_j[u] = tile < tiles ? 16 * tj + li : 0;
+    ti_i[u] = tile < tiles ? 16 * ti + li : 0;
+  }
   for (int64_t t0 = r0; t0 < r1; t0 += kWgTile) {
     const int nt = (int)(r1 - t0 < kWgTile ? r1 - t0 : kWgTile);
     __syncthreads();
@@ -117,17 +132,12 @@ __global__ __launch_bounds__(kWgThreads) void k_linear_wgrad_part(const float* _
       xs2[rr][i] = rr >= nt ? 0.0f : i < in_dim ? x[(t0 + rr) * in_dim + i] : i == in_dim ? 1.0f : 0.0f;
     }
     __syncthreads();
+#pragma unroll 2
+    for (int s = 0; s < kWgTile / 4; ++s)  // (the wave's tiles interleaved: independent accumulator chains)
 #pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int tile = wave + 4 * u;
-      if (tile < tiles) {
-        const int tj = tile / IT, ti = tile - tj * IT;
-        const int j = 16 * tj + li, i = 16 * ti + li;
-#pragma unroll 4
-        for (int s = 0; s < kWgTile / 4; ++s)
-          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(gs[4 * s + q][j], xs2[4 * s + q][i], acc[u], 0, 0, 0);
-      }
-    }
+      for (int u = 0; u < 5; ++u)
+        if (wave + 4 * u < tiles)
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(gs[4 * s + q][tj_j[u]], xs2[4 * s + q][ti_i[u]], acc[u], 0, 0, 0);
   }
 #pragma unroll
   for (int u = 0; u < 5; ++u) {
