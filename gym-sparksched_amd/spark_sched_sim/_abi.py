@@ -13,6 +13,7 @@ SSIM_ROLLOUT_PREEMPT = 0x2
 SSIM_ROLLOUT_WARMUP = 0x4
 SSIM_ROLLOUT_TEST_REJECT = 0x8  # ssim_decima_rollout test hook
 SSIM_DEBUG_ENGINE, SSIM_DEBUG_DECIMA, SSIM_DEBUG_KAT_BAD = 0, 1, 2  # ssim_debug_set_trace_ex variants
+SSIM_ACT_LEAKY_RELU, SSIM_ACT_TANH = 0, 1  # ssim_mlp3_* activations
 SSIM_ERR_SPACE = 0x1
 SSIM_ERR_KEY = 0x2
 SSIM_ERR_TOO_MANY = 0x4

@@ -61,6 +61,17 @@ def lib() -> ct.CDLL:
     L.ssim_linear_wgrad_parts.restype = i32
     L.ssim_linear_wgrad.argtypes = [vp, vp, vp, vp, ct.c_int64, i32, i32, vp, i32, vp]
     L.ssim_linear_wgrad.restype = ct.c_int
+    L.ssim_mlp3_supported.argtypes = [i32, i32, i32, i32, i32]
+    L.ssim_mlp3_supported.restype = i32
+    L.ssim_mlp3_fwd.argtypes = [vp, vp, i32] + [vp] * 9 + [ct.c_int64, i32, i32, i32, i32, i32, ct.c_float, vp]
+    L.ssim_mlp3_fwd.restype = ct.c_int
+    L.ssim_mlp3_parts.argtypes = [ct.c_int64]
+    L.ssim_mlp3_parts.restype = i32
+    L.ssim_mlp3_partial_floats.argtypes = [ct.c_int64, i32, i32, i32, i32]
+    L.ssim_mlp3_partial_floats.restype = ct.c_int64
+    L.ssim_mlp3_bwd.argtypes = [vp, vp, vp, i32] + [vp] * 14 + [ct.c_int64, i32, i32, i32, i32, i32, ct.c_float, vp,
+                                                                 i32, vp]
+    L.ssim_mlp3_bwd.restype = ct.c_int
     for name in ("ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
                  "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
                  "ssim_job_times", "ssim_decima_features", "ssim_decima_policy", "ssim_decima_rollout"):
@@ -80,7 +91,8 @@ EXPORTED_SYMBOLS = ["ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_rese
                     "ssim_decima_features", "ssim_decima_policy", "ssim_decima_workspace_bytes", "ssim_decima_rollout",
                     "ssim_last_error", "ssim_build_id", "ssim_debug_set_trace", "ssim_debug_set_trace_ex",
                     "ssim_debug_kernel_name", "ssim_linear_fwd",
-                    "ssim_linear_wgrad_parts", "ssim_linear_wgrad"]
+                    "ssim_linear_wgrad_parts", "ssim_linear_wgrad", "ssim_mlp3_supported", "ssim_mlp3_fwd",
+                    "ssim_mlp3_parts", "ssim_mlp3_partial_floats", "ssim_mlp3_bwd"]
 
 
 def build_id() -> str:

@@ -37,7 +37,7 @@ import torch.nn as nn
 
 from .. import _abi
 
-from .linear import HipLinear  # noqa: E402
+from .linear import HipLinear, HipMlp3  # noqa: E402
 
 NUM_NODE_FEATURES = 5  # env_wrapper.py:9
 NUM_DAG_FEATURES = 3   # scheduler.py:34
@@ -48,7 +48,7 @@ def make_mlp(input_dim: int, hid_dims: list[int], output_dim: int, act_cls: str,
              act_kwargs: dict[str, Any] | None = None) -> nn.Sequential:
     """schedulers/decima/utils.py:51-70."""
     act = getattr(torch.nn.modules.activation, act_cls)
-    mlp = nn.Sequential()
+    mlp = HipMlp3()  # an nn.Sequential; on the device the two-hidden-layer shapes run as one fused chain
     prev = input_dim
     dims = list(hid_dims) + [output_dim]
     for i, d in enumerate(dims):
@@ -528,9 +528,7 @@ class ExecPolicyNetwork(nn.Module):
         K = dags.numel()
         x_dag = b.x[b.ptr[dags], : self.num_dag_features]
         base = torch.cat([x_dag, h["dag"][dags], h["glob"][envs]], dim=1)
-        acts = (torch.arange(N, device=dags.device) / N)
-        inp = torch.cat([base[:, None, :].expand(K, N, base.shape[1]), acts[None, :, None].expand(K, N, 1)], dim=2)
-        scores = self.mlp_score(inp.reshape(K * N, -1)).view(K, N)
+        scores = self.mlp_score.grid(base, N).view(K, N)  # input row (k, a) = [base[k], a / N]
         valid = torch.arange(N, device=dags.device)[None, :] < b.exec_cap[dags][:, None]
         return scores, valid
 

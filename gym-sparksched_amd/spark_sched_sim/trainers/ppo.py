@@ -24,6 +24,8 @@ from __future__ import annotations
 
 from typing import Any
 
+import math
+
 import numpy as np
 import torch
 
@@ -261,12 +263,20 @@ class PPO:
                                         plan)
                 pol_losses.append(info["policy_loss"])
                 ent_losses.append(info["entropy_loss"])
-                kl = float(info["approx_kl_div"])
+                # the gradients (and the clipped total norm) are computed before the approx-KL value is read, so the
+                # forward and backward launches go out in one run and the minibatch makes ONE host sync; the update
+                # itself still happens only when the KL check passes (ppo.py:88-91, then scheduler.py:34-53)
+                norm = self._backward(loss)
+                kl, total = torch.stack([info["approx_kl_div"].float(), norm.float()]).tolist()
                 kls.append(kl)
                 if self.target_kl is not None and kl > 1.5 * self.target_kl:
+                    self.scheduler.optim.zero_grad()
                     cont = False  # ppo.py:88-91
                     break
-                self._update(loss)
+                if not math.isfinite(total):  # clip_grad_norm_(error_if_nonfinite=True)'s error
+                    raise RuntimeError(f"The total norm of order 2.0 for gradients from `parameters` is non-finite, "
+                                       f"so it cannot be clipped ({total})")
+                self._step()
         pl = torch.stack(pol_losses).mean().item()
         el = torch.stack(ent_losses).mean().item()
         return {"policy loss": abs(pl), "entropy": abs(el), "approx kl div": abs(float(np.mean(kls))), "samples": n}
@@ -286,10 +296,24 @@ class PPO:
 
     def _update(self, loss):
         """TrainableScheduler.update_parameters (scheduler.py:34-53)."""
+        total = float(self._backward(loss))
+        if not math.isfinite(total):
+            raise RuntimeError(f"The total norm of order 2.0 for gradients from `parameters` is non-finite, so it "
+                               f"cannot be clipped ({total})")
+        self._step()
+
+    def _backward(self, loss) -> torch.Tensor:
+        """scheduler.py:34-53 up to the optimizer step: backward and the max_grad_norm clip (on the device, no sync);
+        returns the gradients' total norm (device tensor) for the caller's non-finite check."""
         s = self.scheduler
         loss.backward()
+        params = [p for p in s.parameters() if p.grad is not None]
         if s.max_grad_norm:
-            torch.nn.utils.clip_grad_norm_(s.parameters(), s.max_grad_norm, error_if_nonfinite=True)
+            return torch.nn.utils.clip_grad_norm_(params, s.max_grad_norm)
+        return torch.nn.utils.get_total_norm([p.grad for p in params]) if params else loss.new_zeros(())
+
+    def _step(self):
+        s = self.scheduler
         s.optim.step()
         s.optim.zero_grad()
 

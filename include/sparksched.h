@@ -345,6 +345,34 @@ int32_t ssim_linear_wgrad_parts(int64_t rows);
 int ssim_linear_wgrad(const float* gy, const float* x, float* gw, float* gb, int64_t rows, int32_t in_dim,
                       int32_t out_dim, float* partial, int32_t parts, void* stream);
 
+/* The Decima MLPs as one fused chain each (make_mlp with two hidden layers: Linear(d0, d1), act, Linear(d1, d2), act,
+ * Linear(d2, d3); schedulers/decima/utils.py:51-70): the learner's replacement for 5 forward and ~11 backward
+ * per-layer launches. Supported shapes (ssim_mlp3_supported): d0 in 1..64 and (d1, d2, d3, act) = (32, 16, 16,
+ * SSIM_ACT_LEAKY_RELU) (the GNN MLPs) or (64, 64, 1, SSIM_ACT_TANH) (the score MLPs); weights in nn.Linear's
+ * [out][in] layout. Input: x [rows][d0], or (x == NULL) the exec-score grid scheduler.py:355-367 builds: base
+ * [rows / grid_n][d0 - 1] and row r's last column (r % grid_n) / grid_n (the action fraction), so the
+ * [decisions * N][d0] input is never materialised.
+ * ssim_mlp3_fwd writes y and the post-activation hidden rows h1 [rows][d1], h2 [rows][d2] the backward needs (NULL:
+ * inference, not written).
+ * ssim_mlp3_bwd: from gy [rows][d3] and h1 / h2, the pre-activation gradients g1 / g2 (scratch [rows][d1] / [rows][d2]),
+ * the input gradient gx ([rows][d0]; in grid mode [rows / grid_n][d0 - 1], summed over each decision's actions; NULL:
+ * none) and every weight / bias gradient through `partial` (ssim_mlp3_partial_floats floats; parts =
+ * ssim_mlp3_parts(rows)), summed in chunk order: deterministic. Returns 0, or -1 for an unsupported shape. */
+#define SSIM_ACT_LEAKY_RELU 0
+#define SSIM_ACT_TANH 1
+int32_t ssim_mlp3_supported(int32_t d0, int32_t d1, int32_t d2, int32_t d3, int32_t act);
+int ssim_mlp3_fwd(const float* x, const float* base, int32_t grid_n, const float* w0, const float* b0,
+                  const float* w1, const float* b1, const float* w2, const float* b2, float* h1, float* h2, float* y,
+                  int64_t rows, int32_t d0, int32_t d1, int32_t d2, int32_t d3, int32_t act, float slope,
+                  void* stream);
+int32_t ssim_mlp3_parts(int64_t rows);
+int64_t ssim_mlp3_partial_floats(int64_t rows, int32_t d0, int32_t d1, int32_t d2, int32_t d3);
+int ssim_mlp3_bwd(const float* gy, const float* x, const float* base, int32_t grid_n, const float* w0,
+                  const float* w1, const float* w2, const float* h1, const float* h2, float* g1, float* g2, float* gx,
+                  float* gw0, float* gb0, float* gw1, float* gb1, float* gw2, float* gb2, int64_t rows, int32_t d0,
+                  int32_t d1, int32_t d2, int32_t d3, int32_t act, float slope, float* partial, int32_t parts,
+                  void* stream);
+
 /* Identity of this build: a hash of the library's kernel sources and compile definitions (__graft_entry__.build_lib).
  * bench.py quotes PMC traffic only from a PMC summary (profiles/) made with the same build. */
 const char* ssim_build_id(void);

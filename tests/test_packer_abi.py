@@ -75,7 +75,7 @@ def test_reset_sampler_matches_oracle_job_sequence(dataset, seed, cap, limit):
 def _declared_functions():
     src = open(os.path.join(REPO, "include", "sparksched.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(ssim_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(ssim_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_c_abi_library_exports_every_declared_symbol():
