@@ -72,6 +72,8 @@ def lib() -> ct.CDLL:
     L.ssim_mlp3_bwd.argtypes = [vp, vp, vp, i32] + [vp] * 14 + [ct.c_int64, i32, i32, i32, i32, i32, ct.c_float, vp,
                                                                  i32, vp]
     L.ssim_mlp3_bwd.restype = ct.c_int
+    L.ssim_discounted_returns.argtypes = [vp, vp, vp, ct.c_int64, ct.c_int64, i32, vp]
+    L.ssim_discounted_returns.restype = ct.c_int
     for name in ("ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_reset", "ssim_step", "ssim_policy",
                  "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
                  "ssim_job_times", "ssim_decima_features", "ssim_decima_policy", "ssim_decima_rollout"):
@@ -92,7 +94,7 @@ EXPORTED_SYMBOLS = ["ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_rese
                     "ssim_last_error", "ssim_build_id", "ssim_debug_set_trace", "ssim_debug_set_trace_ex",
                     "ssim_debug_kernel_name", "ssim_linear_fwd",
                     "ssim_linear_wgrad_parts", "ssim_linear_wgrad", "ssim_mlp3_supported", "ssim_mlp3_fwd",
-                    "ssim_mlp3_parts", "ssim_mlp3_partial_floats", "ssim_mlp3_bwd"]
+                    "ssim_mlp3_parts", "ssim_mlp3_partial_floats", "ssim_mlp3_bwd", "ssim_discounted_returns"]
 
 
 def build_id() -> str:

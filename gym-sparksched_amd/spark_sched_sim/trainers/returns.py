@@ -32,6 +32,18 @@ class ReturnsCalculator:
         # R_k = sum_{j>=k} r_j exp(-b (t_j - t_k)) with t_j - t_k = sum_{i=k}^{j-1} dt_i; the backward
         # recursion is evaluated exactly as the reference does, one step per column (vectorised over rows).
         decay = torch.exp(-self.beta * 1e-3 * dt)
+        if r.is_cuda and r.dtype in (torch.float64, torch.float32) and decay.dtype == r.dtype:
+            # the same recursion and roundings in one launch (csrc/k_linear.hip) instead of 3 launches per column
+            from .. import native
+
+            r, decay = r.contiguous(), decay.contiguous()
+            out = torch.empty_like(r)
+            with torch.cuda.device(r.device):
+                native.check(native.lib().ssim_discounted_returns(
+                    r.data_ptr(), decay.data_ptr(), out.data_ptr(), r.shape[0], r.shape[1],
+                    int(r.dtype == torch.float64), torch.cuda.current_stream(r.device).cuda_stream),
+                    "ssim_discounted_returns")
+            return out
         out = torch.zeros_like(r)
         R = torch.zeros_like(r[:, 0])
         for k in range(r.shape[1] - 1, -1, -1):
@@ -83,12 +95,15 @@ class Baseline:
         """times/returns [S*R, T] (rows of a sequence contiguous), lengths [S*R] -> baselines [S*R, T]."""
         Sq, Rr = self.num_sequences, self.num_rollouts
         T = times.shape[1]
-        out = torch.zeros_like(returns)
-        for s in range(Sq):
-            rows = slice(s * Rr, (s + 1) * Rr)
-            ts, ys, n = times[rows], returns[rows], lengths[rows]
-            acc = torch.zeros_like(ys)
-            for r2 in range(Rr):  # evaluate rollout r2's curve at every rollout's own times
-                acc += interp(ts, ts[r2:r2 + 1].expand(Rr, T), ys[r2:r2 + 1].expand(Rr, T), n[r2:r2 + 1].expand(Rr))
-            out[rows] = acc / Rr
-        return out
+        # every (sequence s, rollout r, curve r2) row at once: rollout r2's curve evaluated at rollout r's times
+        # (interp is row-independent), then summed over r2 in the reference's order
+        ts, ys, n = times.view(Sq, Rr, T), returns.view(Sq, Rr, T), lengths.view(Sq, Rr)
+        q = ts[:, :, None, :].expand(Sq, Rr, Rr, T).reshape(-1, T)
+        xp = ts[:, None, :, :].expand(Sq, Rr, Rr, T).reshape(-1, T)
+        fp = ys[:, None, :, :].expand(Sq, Rr, Rr, T).reshape(-1, T)
+        nn_ = n[:, None, :].expand(Sq, Rr, Rr).reshape(-1)
+        v = interp(q, xp, fp, nn_).view(Sq, Rr, Rr, T)
+        acc = torch.zeros_like(v[:, :, 0])
+        for r2 in range(Rr):
+            acc += v[:, :, r2]
+        return (acc / Rr).reshape(Sq * Rr, T)

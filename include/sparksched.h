@@ -373,6 +373,12 @@ int ssim_mlp3_bwd(const float* gy, const float* x, const float* base, int32_t gr
                   int32_t d1, int32_t d2, int32_t d3, int32_t act, float slope, float* partial, int32_t parts,
                   void* stream);
 
+/* Continuously discounted returns (trainers/utils/returns_calculator.py:37-52): out[i][k] = r[i][k] + decay[i][k] *
+ * out[i][k + 1] (out[i][cols] = 0) for row-major [rows][cols] arrays of doubles (f64 != 0) or floats, with the
+ * reference's roundings (product, then sum): bit-identical to its per-column recursion. */
+int ssim_discounted_returns(const void* r, const void* decay, void* out, int64_t rows, int64_t cols, int32_t f64,
+                            void* stream);
+
 /* Identity of this build: a hash of the library's kernel sources and compile definitions (__graft_entry__.build_lib).
  * bench.py quotes PMC traffic only from a PMC summary (profiles/) made with the same build. */
 const char* ssim_build_id(void);

@@ -49,6 +49,22 @@ def main():
         torch.cuda.synchronize()
     print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=25))
     print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=15))
+    if os.environ.get("LEARNER_STACKS"):  # which source lines issue the most device ops (launch-count hunting)
+        ppo.scheduler.load_state_dict(state)
+        ppo.scheduler.optim.load_state_dict(opt_state)
+        with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+            ppo.train_on_rollouts(buf)
+            torch.cuda.synchronize()
+        rows = []
+        for e in prof.key_averages(group_by_stack_n=4):
+            if e.key.startswith("aten::") and e.count >= 300 and e.key not in ("aten::empty", "aten::view",
+                                                                             "aten::as_strided", "aten::select",
+                                                                             "aten::slice", "aten::reshape",
+                                                                             "aten::_reshape_alias", "aten::expand"):
+                stack = " <- ".join(s for s in e.stack if "spark_sched_sim" in s or "ppo" in s)
+                rows.append((e.count, e.key, stack))
+        for c, k, s in sorted(rows, reverse=True)[:45]:
+            print(f"{c:7d} {k:28s} {s}")
 
 
 if __name__ == "__main__":

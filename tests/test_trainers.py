@@ -793,3 +793,30 @@ def test_gpu_learner_matches_cpu_learner(gpu_device, dataset):
         assert rel <= 2e-3, f"{name}: max |gpu - cpu| / max |cpu| = {rel:.2e}"
     print(f"GPU vs CPU learner over {n} samples: first-minibatch gradients worst {worst_g:.2e}, parameters after the "
           f"pass worst {worst:.2e} (per-tensor, relative to the tensor's scale)")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("R,T", [(1, 1), (3, 7), (16, 8193), (5, 0)])
+def test_discounted_returns_kernel_is_bit_exact(gpu_device, dtype, R, T):
+    """ssim_discounted_returns (one launch) against the per-column recursion `R = r[:, k] + decay[:, k] * R`
+    (returns_calculator.py:37-52) on the CPU, from the same r and decay: bit for bit, ragged widths included. (The
+    whole ReturnsCalculator on the device also takes torch's device exp for the decay, checked against the reference
+    at 1e-12 in test_ppo_decima_tpch_iteration_gpu.)"""
+    from spark_sched_sim import native
+
+    g = torch.Generator().manual_seed(R * 1000 + T)
+    r = (-torch.rand(R, T, generator=g, dtype=torch.float64) * 3e4).to(dtype)
+    decay = torch.exp(-5e-6 * torch.rand(R, T, generator=g, dtype=torch.float64) * 5e4).to(dtype)
+    ref = torch.zeros_like(r)
+    acc = torch.zeros(R, dtype=dtype)
+    for k in range(T - 1, -1, -1):
+        acc = r[:, k] + decay[:, k] * acc
+        ref[:, k] = acc
+    rd, dd = r.to(gpu_device), decay.to(gpu_device)
+    out = torch.full_like(rd, float("nan"))
+    native.check(native.lib().ssim_discounted_returns(rd.data_ptr(), dd.data_ptr(), out.data_ptr(), R, T,
+                                                      int(dtype == torch.float64),
+                                                      torch.cuda.current_stream().cuda_stream), "returns")
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref)
