@@ -511,11 +511,13 @@ template <class T>
 __device__ __forceinline__ T ret_step(T r, T d, T R);
 template <>
 __device__ __forceinline__ double ret_step<double>(double r, double d, double R) {
-  return __dadd_rn(r, __dmul_rn(d, R));
+#pragma clang fp contract(off)
+  return r + d * R;  // (contraction off: __dmul_rn / __dadd_rn alone still fused into an fma)
 }
 template <>
 __device__ __forceinline__ float ret_step<float>(float r, float d, float R) {
-  return __fadd_rn(r, __fmul_rn(d, R));
+#pragma clang fp contract(off)
+  return r + d * R;
 }
 
 template <class T>

@@ -103,7 +103,7 @@ def test_hipmlp3_on_cpu_is_the_sequential():
 
 
 def _kinks_masked(ref, x, g):
-    """The upstream gradient with the rows zeroed whose hidden pre-activations lie within 1e-4 of LeakyReLU's kink:
+    """The upstream gradient with the rows zeroed whose hidden pre-activations lie within 2e-5 of LeakyReLU's kink:
     there a different fp32 summation order can pick the other slope (1 vs 0.2), a legitimate difference that says
     nothing about the kernel. Zeroed rows contribute to no gradient in either implementation."""
     if not isinstance(ref[1], torch.nn.LeakyReLU) or x.shape[0] == 0:
@@ -111,8 +111,8 @@ def _kinks_masked(ref, x, g):
     with torch.no_grad():
         pre1 = ref[0](x)
         pre2 = ref[2](torch.nn.functional.leaky_relu(pre1, ref[1].negative_slope))
-        kink = (pre1.abs() < 1e-4).any(1) | (pre2.abs() < 1e-4).any(1)
-    assert float(kink.float().mean()) < 1e-2
+        kink = (pre1.abs() < 2e-5).any(1) | (pre2.abs() < 2e-5).any(1)
+    assert float(kink.float().mean()) < 5e-2
     return g.masked_fill(kink[:, None], 0.0)
 
 
