@@ -324,3 +324,4 @@ struct DecimaRolloutSet {
 DecimaRolloutSet decima_rollout_hbm();    // k_dr_hbm.hip
 DecimaRolloutSet decima_rollout_hbm50();  // k_dr_hbm50.hip: 50 executors / 200 jobs
 DecimaRolloutSet decima_rollout_lds();    // k_dr_lds.hip
+DecimaRolloutSet decima_rollout_lds50();  // k_dr_lds50.hip: 50 executors / 200 jobs

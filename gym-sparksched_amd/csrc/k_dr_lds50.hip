@@ -1,0 +1,8 @@
+// k_dr_lds50.hip — persistent Decima rollout (decima_rollout.h): hot block LDS-resident, specialised on the
+// config/decima_tpch.yaml env (50 executors / 200 jobs): the 16 envs of a PPO iteration (configs[4]), one env per CU.
+#include "decima_rollout.h"
+
+DecimaRolloutSet decima_rollout_lds50() {
+  return {k_decima_rollout<true, 50, 200>, k_decima_rollout_warmup<true, 50, 200>,
+          k_set_trace<WaveHip, true, 50, 200, 0, kTagDrLds50>, "dr_lds50"};
+}

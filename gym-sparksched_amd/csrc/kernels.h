@@ -237,7 +237,7 @@ inline KernelSet kernel_set(const char* name) {
 }
 // Translation-unit tags of k_set_trace (one per k_*.hip)
 enum : int { kTagBench900 = 1, kTagBench, kTagLds, kTagHbm, kTagHbmN100, kTagHbmN10, kTagHbmN50, kTagDrHbm, kTagDrHbm50,
-             kTagDrLds, kTagKatBad };
+             kTagDrLds, kTagKatBad, kTagDrLds50 };
 SetTraceFn set_trace_kat_bad();  // k_hbm_n100.hip: the N = 100 / J = 200 instantiation on WaveHipKatBadPage
 // one per translation unit
 KernelSet kernels_bench900();  // k_bench900.hip: LDS-resident, 10 executors / 50 jobs / stage cap 900

@@ -141,7 +141,8 @@ static KernelSet pick_kernels(const Params& p) {
   return kernels_lds();
 }
 static DecimaRolloutSet pick_decima(const Params& p) {
-  return p.O.lds_resident                          ? decima_rollout_lds()
+  return p.O.lds_resident                          ? (decima_shape(p) && !generic_forced() ? decima_rollout_lds50()
+                                                                                          : decima_rollout_lds())
          : !decima_shape(p) || generic_forced()   ? decima_rollout_hbm()
                                                   : decima_rollout_hbm50();
 }

@@ -100,7 +100,7 @@ def test_cpython_reference_grows_and_churns_tables():
 _HBM, _ENG, _DEC = 1, 0, 1  # _abi.SSIM_CFG_FORCE_HBM, SSIM_DEBUG_ENGINE, SSIM_DEBUG_DECIMA
 SHIPPED = [(10, 50, 0, _ENG, "bench900", 8, 400), (10, 50, _HBM, _ENG, "hbm_n10", 8, 400),
            (50, 200, _HBM, _ENG, "hbm_n50", 10, 600), (50, 200, _HBM, _DEC, "dr_hbm50", 10, 600),
-           (100, 200, _HBM, _ENG, "hbm_n100", 12, 900)]
+           (100, 200, _HBM, _ENG, "hbm_n100", 12, 900), (50, 200, 0, _DEC, "dr_lds50", 10, 600)]
 
 
 def _run_traces(eng, n_exec, traces, n_ops, variant, stop_at_first=False):
