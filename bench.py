@@ -239,6 +239,15 @@ def cpu_baseline(workload: str, seconds: float, procs: int, warm_s: float = 5.0,
                       "(an upper bound for the whole host)"}
 
 
+def add_ratios(cb: dict, gpu_value: float) -> dict:
+    """The north-star ratio read straight off the line: this run's GPU rate over the CPU path measured on the cores
+    used (`ratio_measured`) and over that path projected to every CPU of the host (`ratio_projected_host`). Both are
+    for the GPUs this line measured; a node-level (8-GPU) ratio needs the driver's own 8-GPU line."""
+    cb["ratio_measured"] = gpu_value / cb["value"] if cb.get("value") else None
+    cb["ratio_projected_host"] = gpu_value / cb["projected_host"] if cb.get("projected_host") else None
+    return cb
+
+
 # ------------------------------------------------------------------------------------------------ PMC lookup
 def pmc_traffic(kernel: str, mode: str, envs: int, steps_per_launch: int, decisions_per_launch: float,
                 dataset_seed: int = 0, build_id: str | None = None):
@@ -336,6 +345,7 @@ def run_ppo(args, rank, world, local, dev):
             # learner's time is excluded)
             line["cpu_baseline"] = cpu_baseline("decima", args.cpu_seconds, B)
             line["cpu_baseline"]["sample"] += "; rollout phase of the PPO iteration only (learner excluded)"
+            add_ratios(line["cpu_baseline"], line["value"])
     return line
 
 
@@ -648,6 +658,7 @@ def main():
         if not args.no_cpu_baseline and world == 1 and not host and args.workload in ("tpch", "large", "decima"):
             procs = args.cpu_procs or usable_cpus()
             line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, procs, ds_seed=args.dataset_seed)
+            add_ratios(line["cpu_baseline"], value)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

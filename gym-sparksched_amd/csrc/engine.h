@@ -104,6 +104,12 @@ enum : int32_t { kPhPolicy = 0, kPhAction, kPhRoundCheck, kPhFulfill, kPhPop, kP
 #ifndef SSIM_POOL_STAT
 #define SSIM_POOL_STAT(op, size, used) (void)0
 #endif
+// Diagnostic host build only (scripts/field_stats.py): a hook per wave-uniform read of a hot-block field or record, by
+// section (0 stage field, 1 job field, 2 job times, 3 executor field, 4 executor event field, 5 pool cfrom, 6 stage
+// recent duration, 10 pool record, 11 stage record, 12 executor record, 13 commitment scan step).
+#ifndef SSIM_FIELD_STAT
+#define SSIM_FIELD_STAT(sec) (void)0
+#endif
 enum : int32_t { kPoolNone = -1, kPoolCommon = 0 };
 // trace-only kinds: a job completion (:682-697) and an executor released to the common pool (:779-782, the
 // reference's Executor.add_history(wall, -1)); with the kEvReady records they give the render history.
@@ -524,19 +530,24 @@ struct Sim {
   //    through W::uni, so the value lands in an SGPR and the code that uses it is scalar;
   //  * lane-parallel loops (index differs per lane): read whole records by value (stage(g), job(j),
   //    exr(e) ...) — never through UF, whose readfirstlane would broadcast lane 0's value.
-  template <class T>
+  template <class T, int kSec = -1>
   struct UF {
     T* p;
-    __device__ __forceinline__ operator T() const { return W::uni(*p); }
+    __device__ __forceinline__ operator T() const {
+      SSIM_FIELD_STAT(kSec);
+      return W::uni(*p);
+    }
     __device__ __forceinline__ UF& operator=(T v) {
       *p = v;
       return *this;
     }
     __device__ __forceinline__ UF& operator+=(int v) {
+      SSIM_FIELD_STAT(kSec);
       *p = (T)(*p + v);
       return *this;
     }
     __device__ __forceinline__ UF& operator-=(int v) {
+      SSIM_FIELD_STAT(kSec);
       *p = (T)(*p - v);
       return *this;
     }
@@ -572,38 +583,38 @@ struct Sim {
   __device__ __forceinline__ PoolRec& pool(int p) const { return H<PoolRec>(O.pools)[p]; }
   __device__ __forceinline__ double* recent() const { return reinterpret_cast<double*>(cold + O.st_recent); }
   // stages (env-global index g = job base + local stage id); `done` is derived: rem + exe + done = tasks
-  __device__ __forceinline__ UF<int16_t> st_job(int g) const { return {&stage(g).job}; }
-  __device__ __forceinline__ UF<int16_t> st_ts(int g) const { return {&stage(g).ts}; }
-  __device__ __forceinline__ UF<int16_t> st_rem(int g) const { return {&stage(g).rem}; }
-  __device__ __forceinline__ UF<int16_t> st_exe(int g) const { return {&stage(g).exe}; }
-  __device__ __forceinline__ UF<int16_t> st_mov(int g) const { return {&stage(g).mov}; }
-  __device__ __forceinline__ UF<int16_t> st_com(int g) const { return {&stage(g).com}; }
-  __device__ __forceinline__ UF<int8_t> st_unmet(int g) const { return {&stage(g).unmet}; }
-  __device__ __forceinline__ UF<uint8_t> st_sel(int g) const { return {&stage(g).sel}; }
-  __device__ __forceinline__ UF<double> st_recent(int g) const { return {recent() + g}; }
+  __device__ __forceinline__ UF<int16_t, 0> st_job(int g) const { return {&stage(g).job}; }
+  __device__ __forceinline__ UF<int16_t, 0> st_ts(int g) const { return {&stage(g).ts}; }
+  __device__ __forceinline__ UF<int16_t, 0> st_rem(int g) const { return {&stage(g).rem}; }
+  __device__ __forceinline__ UF<int16_t, 0> st_exe(int g) const { return {&stage(g).exe}; }
+  __device__ __forceinline__ UF<int16_t, 0> st_mov(int g) const { return {&stage(g).mov}; }
+  __device__ __forceinline__ UF<int16_t, 0> st_com(int g) const { return {&stage(g).com}; }
+  __device__ __forceinline__ UF<int8_t, 0> st_unmet(int g) const { return {&stage(g).unmet}; }
+  __device__ __forceinline__ UF<uint8_t, 0> st_sel(int g) const { return {&stage(g).sel}; }
+  __device__ __forceinline__ UF<double, 6> st_recent(int g) const { return {recent() + g}; }
   __device__ __forceinline__ bool st_completed(int g) const { return st_rem(g) == 0 && st_exe(g) == 0; }
   // jobs
-  __device__ __forceinline__ UF<int16_t> job_tpl(int j) const { return {&job(j).tpl}; }
-  __device__ __forceinline__ UF<int16_t> job_base(int j) const { return {&job(j).base}; }
-  __device__ __forceinline__ UF<int16_t> job_nst(int j) const { return {&job(j).nst}; }
-  __device__ __forceinline__ UF<int16_t> job_nact(int j) const { return {&job(j).nact}; }
-  __device__ __forceinline__ UF<int16_t> job_sat(int j) const { return {&job(j).sat}; }
-  __device__ __forceinline__ UF<int16_t> job_local(int j) const { return {&job(j).local}; }
-  __device__ __forceinline__ UF<int16_t> job_supply(int j) const { return {&job(j).supply}; }
-  __device__ __forceinline__ UF<int16_t> job_state(int j) const { return {&job(j).state}; }
-  __device__ __forceinline__ UF<int32_t> job_arr_dec(int j) const { return {&job(j).arr_dec}; }
-  __device__ __forceinline__ UF<int32_t> job_done_dec(int j) const { return {&job(j).done_dec}; }
-  __device__ __forceinline__ UF<double> job_tarr(int j) const { return {&jtimes(j).tarr}; }
-  __device__ __forceinline__ UF<double> job_tdone(int j) const { return {&jtimes(j).tdone}; }
+  __device__ __forceinline__ UF<int16_t, 1> job_tpl(int j) const { return {&job(j).tpl}; }
+  __device__ __forceinline__ UF<int16_t, 1> job_base(int j) const { return {&job(j).base}; }
+  __device__ __forceinline__ UF<int16_t, 1> job_nst(int j) const { return {&job(j).nst}; }
+  __device__ __forceinline__ UF<int16_t, 1> job_nact(int j) const { return {&job(j).nact}; }
+  __device__ __forceinline__ UF<int16_t, 1> job_sat(int j) const { return {&job(j).sat}; }
+  __device__ __forceinline__ UF<int16_t, 1> job_local(int j) const { return {&job(j).local}; }
+  __device__ __forceinline__ UF<int16_t, 1> job_supply(int j) const { return {&job(j).supply}; }
+  __device__ __forceinline__ UF<int16_t, 1> job_state(int j) const { return {&job(j).state}; }
+  __device__ __forceinline__ UF<int32_t, 1> job_arr_dec(int j) const { return {&job(j).arr_dec}; }
+  __device__ __forceinline__ UF<int32_t, 1> job_done_dec(int j) const { return {&job(j).done_dec}; }
+  __device__ __forceinline__ UF<double, 2> job_tarr(int j) const { return {&jtimes(j).tarr}; }
+  __device__ __forceinline__ UF<double, 2> job_tdone(int j) const { return {&jtimes(j).tdone}; }
   // executors
-  __device__ __forceinline__ UF<int16_t> ex_loc(int e) const { return {&exr(e).loc}; }
-  __device__ __forceinline__ UF<int16_t> ex_job(int e) const { return {&exr(e).job}; }
-  __device__ __forceinline__ UF<int16_t> ex_task(int e) const { return {&exr(e).task}; }
-  __device__ __forceinline__ UF<int16_t> ex_busy(int e) const { return {&exr(e).busy}; }
-  __device__ __forceinline__ UF<double> ev_t(int e) const { return {&exr(e).ev_t}; }
-  __device__ __forceinline__ UF<int32_t> ev_seq(int e) const { return {&exr(e).ev_seq}; }
-  __device__ __forceinline__ UF<int16_t> ev_type(int e) const { return {&exr(e).ev_type}; }
-  __device__ __forceinline__ UF<int16_t> ev_stage(int e) const { return {&exr(e).ev_stage}; }
+  __device__ __forceinline__ UF<int16_t, 3> ex_loc(int e) const { return {&exr(e).loc}; }
+  __device__ __forceinline__ UF<int16_t, 3> ex_job(int e) const { return {&exr(e).job}; }
+  __device__ __forceinline__ UF<int16_t, 3> ex_task(int e) const { return {&exr(e).task}; }
+  __device__ __forceinline__ UF<int16_t, 3> ex_busy(int e) const { return {&exr(e).busy}; }
+  __device__ __forceinline__ UF<double, 4> ev_t(int e) const { return {&exr(e).ev_t}; }
+  __device__ __forceinline__ UF<int32_t, 4> ev_seq(int e) const { return {&exr(e).ev_seq}; }
+  __device__ __forceinline__ UF<int16_t, 4> ev_type(int e) const { return {&exr(e).ev_type}; }
+  __device__ __forceinline__ UF<int16_t, 4> ev_stage(int e) const { return {&exr(e).ev_stage}; }
   // pools: code 0 = COMMON, 1+j = job j, 1+job_cap+g = stage g, -1 = None
   __device__ __forceinline__ int32_t job_pool(int j) const { return 1 + j; }
   __device__ __forceinline__ int32_t stage_pool(int g) const { return 1 + JC + g; }
@@ -616,7 +627,7 @@ struct Sim {
   }
   __device__ __forceinline__ PySetMeta* pmeta(int p) const { return reinterpret_cast<PySetMeta*>(&pool(p)); }
   __device__ __forceinline__ uint8_t* ptab(int p) const { return cold + O.pool_tab + (int64_t)p * tab_stride_for(NE); }
-  __device__ __forceinline__ UF<int16_t> cfrom(int p) const { return {&pool(p).cfrom}; }
+  __device__ __forceinline__ UF<int16_t, 5> cfrom(int p) const { return {&pool(p).cfrom}; }
   __device__ __forceinline__ int pool_size(int p) const { return p < 0 ? 0 : (int)W::uni(pool(p).used); }
 
   // ---------------------------------------------------------------- tracker (executor_tracker.py)
@@ -625,6 +636,7 @@ struct Sim {
   }
   __device__ __forceinline__ int committable() {  // :105-111 (pool None is always empty with no commitments)
     if (h.source < 0) return 0;
+    SSIM_FIELD_STAT(10);
     const PoolRec pr = pool(h.source);  // size and commitments-from in one LDS round trip
     const int n = (int)W::uni(pr.used) - (int)W::uni(pr.cfrom);
     check(n >= 0);
@@ -644,6 +656,7 @@ struct Sim {
     check(src >= 0);
     if (src < 0) return;
     int hit = -1, freeslot = -1;
+    SSIM_FIELD_STAT(13);
     for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
       const int k = k0 + W::lane();
       const bool ok = k < commit_cap_for(NE);
@@ -679,6 +692,7 @@ struct Sim {
   }
 
   __device__ __forceinline__ int find_commit(int src, int dst) {
+    SSIM_FIELD_STAT(13);
     for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
       const int k = k0 + W::lane();
       bool hit = false;
@@ -720,6 +734,7 @@ struct Sim {
 
   __device__ __forceinline__ int peek_commitment(int p) {  // :175-180: first key in insertion order, -1 = None
     int best_ord = 0x7FFFFFFF, best_dst = kPoolNone;
+    SSIM_FIELD_STAT(13);
     for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
       const int k = k0 + W::lane();
       int ord = 0x7FFFFFFF, dst = kPoolNone;
@@ -744,6 +759,7 @@ struct Sim {
     int n = 0, last = -1;
     for (;;) {  // selection by increasing insertion stamp (live entries <= N)
       int ord = 0x7FFFFFFF, k_best = -1;
+      SSIM_FIELD_STAT(13);
       for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
         const int k = k0 + W::lane();
         int o = 0x7FFFFFFF, kk = -1;
@@ -858,6 +874,7 @@ struct Sim {
     int v;
   };
   __device__ __forceinline__ PoolView pool_view(int p) {
+    SSIM_FIELD_STAT(10);
     const PoolRec r = pool(p);
     uint32_t w[4];
     __builtin_memcpy(w, &r, sizeof(w));
@@ -1012,9 +1029,10 @@ struct Sim {
   }
 
   // ---- paged tables (device waves; 64 < set_cap <= 512, i.e. 16..127 executors: configs[2] / [3]) ----
-  // A table of up to 512 slots is held 8 slots per lane, page-major: lane l holds slots l, 64 + l, ..., 448 + l as the
-  // bytes of one 64-bit value (byte g = slot 64g + l), which is also the layout of its cold-block home
-  // (layout.h tab_stride_for), so ONE 8-byte load per lane brings the whole table and a slot write is one byte store.
+  // A table of up to 512 slots is held 8 slots per lane, page-major in registers: lane l holds slots l, 64 + l, ...,
+  // 448 + l as the bytes of one 64-bit value (byte g = slot 64g + l). Its cold-block home keeps slot order (byte s =
+  // slot s, layout.h tab_stride_for), so loading page g is one coalesced 64-B byte load per lane, a table costs its
+  // current size in bytes (not the 512-B capacity) and a slot write is one byte store.
   // A probe window (<= 10 consecutive slots) lies in one page or two adjacent ones: per probe step, ballots of the
   // page's byte (EMPTY / DUMMY / key) give the window's bits with no dependent per-slot loads (the serial form staged
   // the table through LDS and walked it one byte read at a time; N = 100 makes ~18 set operations per decision).
@@ -1034,8 +1052,7 @@ struct Sim {
   };
   __device__ __forceinline__ PagedView paged_view(int p) {
     const int l = W::lane();
-    // the cold home is read speculatively, in parallel with the record (an inline 8-slot table ignores it)
-    const uint64_t cv = *reinterpret_cast<const uint64_t*>(ptab(p) + 8 * l);
+    SSIM_FIELD_STAT(10);
     const PoolRec r = pool(p);
     uint32_t w[4];
     __builtin_memcpy(w, &r, sizeof(w));
@@ -1045,15 +1062,24 @@ struct Sim {
     pv.fill = w0 >> 16;
     pv.used = w1 & 0xFFFFu;
     const uint32_t size = pv.mask + 1;
+    // The cold home is read only once the record says the table lives there, and only its `size` bytes (slot order:
+    // page g is the 64 contiguous bytes at 64g, so lane l's byte load of each page is one coalesced 64-B segment).
+    // An inline 8-slot table (the common case: most stage and job pools) issues no cold read at all.
     if (size == 8) {
       const uint32_t b = ((l < 4 ? w[2] : w[3]) >> (8 * (l & 3))) & 0xFFu;
       pv.v = page_of(l < 8 ? (0xFFFFFF00u | b) : 0xFFFFFFFFu, 0xFFFFFFFFu);
-    } else if (size < 64) {
-      pv.v = page_of(l < (int)size ? (0xFFFFFF00u | ((uint32_t)cv & 0xFFu)) : 0xFFFFFFFFu, 0xFFFFFFFFu);
-    } else {  // pages np.. are EMPTY
+    } else if (size <= 64) {
+      const uint32_t b = l < (int)size ? (uint32_t)ptab(p)[l] : kSlotEmpty;
+      pv.v = page_of(0xFFFFFF00u | b, 0xFFFFFFFFu);
+    } else {  // 2, 4 or 8 pages; pages np.. are EMPTY
+      const uint8_t* t = ptab(p) + l;
       const uint32_t np = size / 64;
-      const uint32_t lo = (uint32_t)cv, hi = (uint32_t)(cv >> 32);
-      pv.v = page_of(np >= 4 ? lo : (lo | (0xFFFFFFFFu << (8 * np))), np >= 8 ? hi : np >= 4 ? (hi | (0xFFFFFFFFu << (8 * (np - 4)))) : 0xFFFFFFFFu);
+      const uint32_t b0 = t[0], b1 = t[64];
+      uint32_t lo = 0xFFFF0000u | (b1 << 8) | b0, hi = 0xFFFFFFFFu;
+      if (np >= 4) lo = ((uint32_t)t[192] << 24) | ((uint32_t)t[128] << 16) | (b1 << 8) | b0;
+      if (np >= 8)
+        hi = ((uint32_t)t[448] << 24) | ((uint32_t)t[384] << 16) | ((uint32_t)t[320] << 8) | (uint32_t)t[256];
+      pv.v = page_of(lo, hi);
     }
     return pv;
   }
@@ -1134,7 +1160,7 @@ struct Sim {
       if (mask == 7)
         pool(p).tab[slot] = (uint8_t)val;
       else
-        ptab(p)[8 * (slot & 63) + (slot >> 6)] = (uint8_t)val;
+        ptab(p)[slot] = (uint8_t)val;
     }
     W::sync();
   }
@@ -1143,10 +1169,23 @@ struct Sim {
     W::sync();
     if (size == 8) {
       if (l < 8) pool(p).tab[l] = (uint8_t)v;
-    } else if (size < 64) {
-      if (l < (int)size) ptab(p)[8 * l] = (uint8_t)v;
-    } else {
-      *reinterpret_cast<uint64_t*>(ptab(p) + 8 * l) = v;
+    } else if (size <= 64) {
+      if (l < (int)size) ptab(p)[l] = (uint8_t)v;
+    } else {  // page g of this lane's register copy to byte 64g + l
+      uint8_t* t = ptab(p) + l;
+      const uint32_t np = size / 64, lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+      t[0] = (uint8_t)lo;
+      t[64] = (uint8_t)(lo >> 8);
+      if (np >= 4) {
+        t[128] = (uint8_t)(lo >> 16);
+        t[192] = (uint8_t)(lo >> 24);
+      }
+      if (np >= 8) {
+        t[256] = (uint8_t)hi;
+        t[320] = (uint8_t)(hi >> 8);
+        t[384] = (uint8_t)(hi >> 16);
+        t[448] = (uint8_t)(hi >> 24);
+      }
     }
     W::sync();
   }
@@ -1744,6 +1783,7 @@ struct Sim {
     ev_regs_set(e, x.ev_t, x.ev_seq, kEvTask, g);
   }
   __device__ __forceinline__ void run_next_task(int e, int g) {  // :584-615
+    SSIM_FIELD_STAT(11);
     const StageRec sraw = stage(g);  // both records in one LDS round trip
     const ExecRec xraw = exr(e);
     StageRec s = ld_rec(sraw);
@@ -1797,6 +1837,7 @@ struct Sim {
 
   __device__ __forceinline__ void goto_stage(int e, int g) {  // _move_executor_to_stage :799-819 (+ backup loop)
     for (int guard = 0; guard < 4 * SC + 8; ++guard) {
+      SSIM_FIELD_STAT(11);
       const StageRec sraw = stage(g);  // the stage record and the executor's job in one LDS round trip
       const int16_t xjob = exr(e).job;
       const StageRec sr = ld_rec(sraw);
@@ -1915,6 +1956,7 @@ struct Sim {
   }
 
   __device__ __forceinline__ void on_executor_arrival(int e, int g) {  // :440-450
+    SSIM_FIELD_STAT(11);
     const StageRec sraw = stage(g);  // stage and executor records in one LDS round trip
     const ExecRec xraw = exr(e);
     const StageRec sr = ld_rec(sraw);
@@ -2121,6 +2163,7 @@ struct Sim {
         } else {
           // the stage and executor records (and the cached duration descriptors) are read together (one LDS round
           // trip), then made uniform
+          SSIM_FIELD_STAT(11);
           const StageRec sraw = stage(g);
           const ExecRec xraw = exr(e);
           DurDesc ddc{0, 0};

@@ -186,8 +186,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
 // [n_ops][6] = (code, key, busy bitmap words 0..3); code 0 add(key), 1 remove(key), 2 idle order:
 // list(set(e for e in s.copy() if not busy[e])) with the executors' busy flags from the bitmap. orders [n_ops][width]:
 // the set's iteration order after an add / remove, the idle order for code 2; -1 padded. Clobbers env 0.
+// Compiled under the rollout kernels' occupancy attribute (the same register budget), but as its own kernel: it pins
+// the set code's logic per unit and its codegen at that budget, not the inlined codegen inside k_rollout /
+// k_decima_rollout (those are pinned end to end by the replay tests).
 template <class WV, bool kRes, int kN, int kJ, int kS, int kTag>
-__global__ __launch_bounds__(64) void k_set_trace(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_ROLLOUT_WAVES(kRes)))) void k_set_trace(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                   const int32_t* __restrict__ ops, int n_ops, int width,
                                                   int32_t* orders) {
   Sim<WV, kN, kJ, kS> s(P, state, g_smem, obs, 0, kRes);

@@ -152,6 +152,7 @@ static_assert(sizeof(TraceRec) == kTraceBytes, "trace record size");
 struct StateOffsets {
   int64_t hot_bytes, cold_bytes, scratch_bytes, env_bytes;
   int64_t lds_bytes;        // scratch (+ hot when LDS-resident); decided by compute_layout
+  int64_t lds_share;        // LDS per env that keeps the workgroups per CU the residency decision assumed
   int32_t lds_resident, row_of_lds;  // row_of_lds: observe()'s stage -> row map in the LDS scratch (sc_row_of)
   int64_t hdr, acc, jobs, jtimes, active_jobs, execs, sel_list, commits, stages, pools, active_stages,
       sched_list;
@@ -170,14 +171,12 @@ constexpr int set_cap_for(int n) {  // smallest power of two > 4N (max CPython s
   return c;
 }
 constexpr int commit_cap_for(int n) { return 2 * n + 2; }
-// Bytes per pool in the cold block's table area. Tables of up to 512 slots (executor counts 16..127) are stored
-// page-major for the device's lane-parallel set operations (engine.h "paged tables": slot s at byte
-// 8 * (s % 64) + s / 64, so lane l reads its 8 slots with one 8-byte load), which takes the full 512 bytes whatever
-// the current capacity; smaller and larger capacities keep slot order (byte s = slot s).
+// Bytes per pool in the cold block's table area: the largest table N executors can need, in slot order (byte s =
+// slot s). The device's lane-parallel set operations for 16..127 executors (engine.h "paged tables", up to 512 slots)
+// load page g as the 64 bytes at 64g, so an operation reads the table's current size, not its capacity. (Round 5
+// stored these tables page-major at a 512-B stride for every N, so each operation fetched 512 B whatever the size.)
 constexpr int kPagedTabMax = 512;
-constexpr int tab_stride_for(int n) {
-  return set_cap_for(n) > 64 && set_cap_for(n) <= kPagedTabMax ? kPagedTabMax : set_cap_for(n);
-}
+constexpr int tab_stride_for(int n) { return set_cap_for(n); }
 constexpr int64_t kDurCacheMaxExecs = 16;
 
 // The per-env block layout as a function of (N, J, S). Single source of truth for the host layout and for
@@ -292,6 +291,17 @@ inline bool compute_layout(const ssim_config& cfg, ssim_layout* L, StateOffsets*
   O->lds_bytes = O->lds_resident ? O->hot_bytes + O->scratch_bytes
                                  : O->row_of_lds ? O->scratch_bytes : O->scratch_hbm_bytes;
   L->lds_bytes = O->lds_bytes;
+  // The env's share of its CU's LDS: what may be added on top of lds_bytes (the Decima rollout's policy plan) without
+  // lowering the concurrency the residency decision counted on. LDS-resident: up to 4 envs per CU (lds_concurrent_envs);
+  // a batch of at most one env per CU may take the whole CU. HBM-resident: 16 one-wave workgroups per CU.
+  if (O->lds_resident) {
+    const int64_t per_cu = lds_concurrent_envs(need, chip_cus) / (chip_cus > 0 ? chip_cus : 1);
+    O->lds_share = B <= chip_cus ? kLdsBudgetBig : kLdsPerCu / (per_cu > 1 ? per_cu : 1);
+  } else {
+    O->lds_share = kLdsPerCu / kHbmWorkgroupsPerCu;
+  }
+  L->lds_share = O->lds_share;
+  L->chip_cus = chip_cus;
 
   // obs arena: each field is [B][per-env]
   int64_t b = 0;

@@ -581,6 +581,47 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
   return hip_check(hipGetLastError(), "k_decima_policy launch");
 }
 
+// The persistent Decima rollout's LDS plan (decima_rollout.h): the policy's per-node rows for observations of up to
+// `cap` nodes in the wave's LDS, after the engine's own LDS (`off` relative to the scratch block), within the env's
+// share of its CU (StateOffsets::lds_share: the share compute_layout's residency decision assumed, so the plan never
+// lowers the workgroups per CU the layout counted on).
+struct DecimaLdsPlan {
+  int32_t cap, off;
+  int64_t lds;  // dynamic LDS of the launch
+};
+static DecimaLdsPlan decima_lds_plan(const Params& P) {
+  const StateOffsets& O = P.O;
+  const ssim_layout& L = P.L;
+  DecimaLdsPlan pl{0, 0, O.lds_bytes};
+  const int64_t eng = O.lds_resident ? O.hot_bytes + O.scratch_bytes : O.scratch_hbm_bytes;  // (HBM: row map cold)
+  // HBM-resident engines without the duration-descriptor cache hold only per-operation temporaries in their LDS
+  // scratch (set tables, key lists, the commitment plan), none live across a decision: the plan overlays them.
+#ifdef SSIM_PROFILE
+  const bool overlay = false;  // (the profile sums live in the scratch)
+#else
+  const bool overlay = !O.lds_resident && L.num_executors > kDurCacheMaxExecs;
+#endif
+  const int64_t off = overlay ? 0 : align16(O.lds_resident ? O.scratch_bytes : O.scratch_hbm_bytes);
+  const int64_t base = O.lds_resident ? O.hot_bytes : 0;  // (the plan offset is relative to the scratch block)
+  const int64_t room = O.lds_share - base - off;
+  int cap = 0;
+  while (cap < L.stage_cap && decima_policy_lds_bytes(cap + 1, kDpLdsDags) <= room &&
+         decima_scratch_bytes(cap + 1) <= room)
+    ++cap;
+  pl.cap = cap;
+  pl.off = (int32_t)off;
+  if (cap > 0) {
+    const int64_t need = base + off + decima_policy_lds_bytes(cap, kDpLdsDags);
+    pl.lds = need > align16(eng) ? need : align16(eng);
+  }
+  return pl;
+}
+
+extern "C" int64_t ssim_decima_rollout_lds_bytes(const ssim_handle* h) {
+  if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_decima_rollout_lds_bytes: null handle");
+  return decima_lds_plan(h->params).lds;
+}
+
 extern "C" int64_t ssim_decima_workspace_bytes(const ssim_handle* h) {
   if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_decima_workspace_bytes: null handle");
   return decima_work(h->params.L).total;
@@ -633,32 +674,10 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
   }
   const DecimaRolloutSet ks = pick_decima(h->params);
   const DecimaRolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
-  int64_t lds = h->params.O.lds_bytes;
-  {  // the LDS plan: the CU's LDS share (decima_rollout.h)
-    const StateOffsets& O = h->params.O;
-    const int64_t eng = O.lds_resident ? O.hot_bytes + O.scratch_bytes : O.scratch_hbm_bytes;  // (HBM: row map cold)
-    const int64_t budget = O.lds_resident ? kLdsBudgetBig : kLdsPerCu / kHbmWorkgroupsPerCu;
-    // HBM-resident engines without the duration-descriptor cache hold only per-operation temporaries in their LDS
-    // scratch (set tables, key lists, the commitment plan), none live across a decision: the plan overlays them.
-#ifdef SSIM_PROFILE
-    const bool overlay = false;  // (the profile sums live in the scratch)
-#else
-    const bool overlay = !O.lds_resident && L.num_executors > kDurCacheMaxExecs;
-#endif
-    const int64_t off = overlay ? 0 : align16(O.lds_resident ? O.scratch_bytes : O.scratch_hbm_bytes);
-    const int64_t base = O.lds_resident ? O.hot_bytes : 0;  // (the plan offset is relative to the scratch block)
-    const int64_t room = budget - base - off;
-    int cap = 0;
-    while (cap < L.stage_cap && decima_policy_lds_bytes(cap + 1, kDpLdsDags) <= room &&
-           decima_scratch_bytes(cap + 1) <= room)
-      ++cap;
-    a.plan_cap = cap;
-    a.plan_off = (int32_t)off;
-    if (cap > 0) {
-      const int64_t need = base + off + decima_policy_lds_bytes(cap, kDpLdsDags);
-      lds = need > align16(eng) ? need : align16(eng);
-    }
-  }
+  const DecimaLdsPlan pl = decima_lds_plan(h->params);
+  a.plan_cap = pl.cap;
+  a.plan_off = pl.off;
+  const int64_t lds = pl.lds;
   const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   if (total_decisions > 0 && h->ticket_slot) flags |= kFlagTicketSlot;

@@ -104,7 +104,7 @@ class SsimLayout(ct.Structure):
         "trace_cap", "lds_resident")] + [(n, ct.c_int64) for n in (
         "env_bytes", "state_bytes", "obs_bytes", "reset_bytes", "reset_stride", "scratch_bytes",
         "ob_nodes", "ob_edge_links", "ob_dag_ptr", "ob_supplies", "ob_frontier", "ob_sched_rank", "ob_counts",
-        "ob_reward", "ob_wall_time", "ob_acc", "ob_trace", "lds_bytes")]
+        "ob_reward", "ob_wall_time", "ob_acc", "ob_trace", "lds_bytes", "lds_share", "chip_cus")]
 
 
 class SsimDecimaSamples(ct.Structure):

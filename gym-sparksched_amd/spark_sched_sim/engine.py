@@ -202,8 +202,14 @@ class DeviceEngine:
         self.packed = packed.with_executors(N)
         self.cfg = make_config(env_cfg, num_envs, self.packed, job_cap, trace_cap, config_flags)
         self.num_envs = num_envs
+        # the library sizes LDS residency from the CURRENT device's compute units (ssim_layout.chip_cus): make it this
+        # engine's device for the layout query and ssim_create
+        import contextlib
+
+        on_dev = torch.cuda.device(self.device) if self.device.type == "cuda" else contextlib.nullcontext()
         L = SsimLayout()
-        native.check(native.lib().ssim_layout_for(ct.byref(self.cfg), ct.byref(L)), "ssim_layout_for")
+        with on_dev:
+            native.check(native.lib().ssim_layout_for(ct.byref(self.cfg), ct.byref(L)), "ssim_layout_for")
         self.layout = L
         # dataset blob
         arrays = self.packed.arrays()
@@ -224,9 +230,10 @@ class DeviceEngine:
         self.reset_host = np.zeros(L.reset_bytes, dtype=np.uint8)
         self.actions = torch.zeros((2, num_envs), dtype=torch.int32, device=self.device)
         h = ct.c_void_p()
-        native.check(native.lib().ssim_create(ct.byref(self.cfg), ct.byref(self.ds), self.state.data_ptr(),
-                                              self.obs.data_ptr(), self.reset_dev.data_ptr(), ct.byref(h)),
-                     "ssim_create")
+        with on_dev:
+            native.check(native.lib().ssim_create(ct.byref(self.cfg), ct.byref(self.ds), self.state.data_ptr(),
+                                                  self.obs.data_ptr(), self.reset_dev.data_ptr(), ct.byref(h)),
+                         "ssim_create")
         self.handle = h
         self.views = arena_views(self.obs, L)
         self.sampler = _ResetSampler(self.env_cfg, self.cfg.job_cap, num_envs)

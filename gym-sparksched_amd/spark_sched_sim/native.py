@@ -45,6 +45,8 @@ def lib() -> ct.CDLL:
     L.ssim_decima_features.argtypes = [vp, ct.c_float, ct.c_float, vp, vp, vp, vp, vp]
     L.ssim_decima_workspace_bytes.argtypes = [vp]
     L.ssim_decima_workspace_bytes.restype = ct.c_int64
+    L.ssim_decima_rollout_lds_bytes.argtypes = [vp]
+    L.ssim_decima_rollout_lds_bytes.restype = ct.c_int64
     L.ssim_decima_rollout.argtypes = [vp, vp, i32, ct.c_float, ct.c_float, u64, u64, i32, ct.c_int64, i32, vp, vp,
                                       ct.c_int64, vp, vp, vp]
     L.ssim_last_error.restype = ct.c_char_p
@@ -91,6 +93,7 @@ EXPORTED_SYMBOLS = ["ssim_layout_for", "ssim_create", "ssim_destroy", "ssim_rese
                     "ssim_rollout", "ssim_rollout_ex", "ssim_rollout_budget", "ssim_rollout_steps", "ssim_reset_sampled",
                     "ssim_job_times",
                     "ssim_decima_features", "ssim_decima_policy", "ssim_decima_workspace_bytes", "ssim_decima_rollout",
+                    "ssim_decima_rollout_lds_bytes",
                     "ssim_last_error", "ssim_build_id", "ssim_debug_set_trace", "ssim_debug_set_trace_ex",
                     "ssim_debug_kernel_name", "ssim_linear_fwd",
                     "ssim_linear_wgrad_parts", "ssim_linear_wgrad", "ssim_mlp3_supported", "ssim_mlp3_fwd",

@@ -273,9 +273,7 @@ class PPO:
                     self.scheduler.optim.zero_grad()
                     cont = False  # ppo.py:88-91
                     break
-                if not math.isfinite(total):  # clip_grad_norm_(error_if_nonfinite=True)'s error
-                    raise RuntimeError(f"The total norm of order 2.0 for gradients from `parameters` is non-finite, "
-                                       f"so it cannot be clipped ({total})")
+                self._clip(norm, total)
                 self._step()
         pl = torch.stack(pol_losses).mean().item()
         el = torch.stack(ent_losses).mean().item()
@@ -296,21 +294,31 @@ class PPO:
 
     def _update(self, loss):
         """TrainableScheduler.update_parameters (scheduler.py:34-53)."""
-        total = float(self._backward(loss))
-        if not math.isfinite(total):
-            raise RuntimeError(f"The total norm of order 2.0 for gradients from `parameters` is non-finite, so it "
-                               f"cannot be clipped ({total})")
+        norm = self._backward(loss)
+        self._clip(norm, float(norm))
         self._step()
 
     def _backward(self, loss) -> torch.Tensor:
-        """scheduler.py:34-53 up to the optimizer step: backward and the max_grad_norm clip (on the device, no sync);
-        returns the gradients' total norm (device tensor) for the caller's non-finite check."""
+        """scheduler.py:34-53 up to the clip: backward, then the gradients' total norm (device tensor, no sync), so the
+        caller can read it together with the approx-KL value in one host sync. The gradients are not modified here."""
         s = self.scheduler
         loss.backward()
         params = [p for p in s.parameters() if p.grad is not None]
-        if s.max_grad_norm:
-            return torch.nn.utils.clip_grad_norm_(params, s.max_grad_norm)
-        return torch.nn.utils.get_total_norm([p.grad for p in params]) if params else loss.new_zeros(())
+        if not s.max_grad_norm or not params:
+            return loss.new_zeros(())
+        return torch.nn.utils.get_total_norm([p.grad for p in params])
+
+    def _clip(self, norm: torch.Tensor, total: float) -> None:
+        """scheduler.py:44-48: with max_grad_norm set, clip_grad_norm_(error_if_nonfinite=True) — a non-finite total norm
+        raises BEFORE any gradient is scaled; without it the reference steps unclipped, whatever the gradients hold."""
+        s = self.scheduler
+        if not s.max_grad_norm:
+            return
+        if not math.isfinite(total):
+            raise RuntimeError(f"The total norm of order 2.0 for gradients from `parameters` is non-finite, so it "
+                               f"cannot be clipped ({total})")
+        params = [p for p in s.parameters() if p.grad is not None]
+        torch.nn.utils.clip_grads_with_norm_(params, s.max_grad_norm, norm)
 
     def _step(self):
         s = self.scheduler

@@ -124,6 +124,10 @@ typedef struct ssim_layout {
                                                       events popped, decisions, finished episodes, 0, 0 */
   int64_t ob_trace;       /* float64/int32 trace records, [trace_cap] x 32 B */
   int64_t lds_bytes;       /* dynamic LDS of one engine workgroup (one env): scratch, plus the hot block if resident */
+  int64_t lds_share;       /* LDS one env may hold without lowering the workgroups per CU the residency decision
+                              assumed (LDS-resident: 160 KB / envs per CU, the whole CU when num_envs <= chip_cus;
+                              HBM-resident: 160 KB / 16); the Decima rollout's policy plan stays within it */
+  int64_t chip_cus;        /* compute units of the device the layout was computed for (current device) */
 } ssim_layout;
 
 /* indices into the per-env int32 counts block */
@@ -256,7 +260,10 @@ int ssim_decima_features(ssim_handle* h, float num_tasks_scale, float work_scale
  * region the handle allocates (and grows) on demand. env_mask (optional uint8 [B]): 0 = skip the env.
  * Outputs [B]: stage_idx (index among schedulable stages, -1 none), num_exec (= 1 + exec_idx), job_idx
  * (active-job index), exec_idx, lgprob (log-probability of both choices); optional stage_scores
- * [B][stage_cap] and exec_scores [B][N] (for checking). */
+ * [B][stage_cap] and exec_scores [B][N] (for checking).
+ * Stream use: each call repacks `params` into ONE handle-owned operand buffer on `stream` before its launch, so calls on
+ * one handle must be ordered on one stream (as every call on a handle is, see ssim_create): two calls on different
+ * streams could overwrite the packed weights while the earlier launch still reads them. */
 int ssim_decima_policy(ssim_handle* h, const float* node_feats, const int32_t* commit_cap, const uint32_t* edge_mask,
                        const int32_t* depth, const float* params, int32_t num_params, int32_t node_cap, uint64_t seed,
                        uint64_t counter, const uint8_t* env_mask, int32_t* stage_idx, int32_t* num_exec,
@@ -292,6 +299,10 @@ typedef struct ssim_decima_samples {
 
 /* Bytes of the per-env workspace ssim_decima_rollout needs for this handle's layout (device memory, caller-owned). */
 int64_t ssim_decima_workspace_bytes(const ssim_handle* h);
+
+/* Dynamic LDS bytes per workgroup (one env) of this handle's ssim_decima_rollout launch: the engine's LDS plus the
+ * policy plan, within the env's share of its compute unit (ssim_layout.lds_share). Diagnostic / sizing query. */
+int64_t ssim_decima_rollout_lds_bytes(const ssim_handle* h);
 
 /* Decima rollouts in one launch. `params`/`num_params` as ssim_decima_policy; num_tasks_scale / work_scale as
  * ssim_decima_features. Each env takes at most `max_steps` decisions. Sampling stream: (seed, env, counter + the env's

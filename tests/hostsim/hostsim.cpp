@@ -26,6 +26,15 @@ static inline void pool_stat(int op, int size, int used) {
 }
 #define SSIM_POOL_STAT(op, size, used) pool_stat(op, size, used)
 #endif
+// Diagnostic variant (-DSSIM_FIELD_STATS, scripts/field_stats.py): wave-uniform hot-block reads by section (engine.h
+// SSIM_FIELD_STAT).
+#ifdef SSIM_FIELD_STATS
+static int64_t g_field[16];
+#define SSIM_FIELD_STAT(sec) \
+  do {                       \
+    if ((sec) >= 0) g_field[(sec)]++; \
+  } while (0)
+#endif
 
 #include "decima.h"
 #include "engine.h"
@@ -276,6 +285,13 @@ void hs_pool_stats(int64_t* out) {  // [3][16] op counts then [3][16] key sums; 
   memcpy(out + 48, g_pool_keys, sizeof(g_pool_keys));
   memset(g_pool_ops, 0, sizeof(g_pool_ops));
   memset(g_pool_keys, 0, sizeof(g_pool_keys));
+}
+#endif
+
+#ifdef SSIM_FIELD_STATS
+void hs_field_stats(int64_t* out) {  // [16] read counts by section; resets the counters
+  memcpy(out, g_field, sizeof(g_field));
+  memset(g_field, 0, sizeof(g_field));
 }
 #endif
 

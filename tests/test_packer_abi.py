@@ -126,12 +126,25 @@ def test_layout_structs_match_header():
         assert (L.lds_bytes == L.scratch_bytes) == row_map_in_lds, (n_exec, L.lds_bytes, L.scratch_bytes)
     # batches past 1.5x the LDS-resident kernel's concurrency (4 configs[1] envs per CU, 1024 on the chip) run on
     # the 4-wave HBM-resident kernels (layout.h lds_concurrent_envs)
-    for envs, resident in ((1024, 1), (1536, 1), (1537, 0), (4096, 0)):
+    # (thresholds from the CU count the library reports: a partitioned device has fewer than the MI355X's 256)
+    cfg.num_envs = 1
+    assert lib.ssim_layout_for(ctypes.byref(cfg), ctypes.byref(L)) == 0
+    cus = int(L.chip_cus)
+    assert cus > 0
+    conc = 4 * cus  # 4 configs[1] envs per CU
+    for envs, resident in ((conc, 1), (conc * 3 // 2, 1), (conc * 3 // 2 + 1, 0), (4 * conc, 0)):
         cfg.num_envs = envs
         assert lib.ssim_layout_for(ctypes.byref(cfg), ctypes.byref(L)) == 0
         assert L.lds_resident == resident, (envs, L.lds_resident)
         if not resident:
             assert 16 * L.lds_bytes <= 160 * 1024, L.lds_bytes
+            assert L.lds_share == 160 * 1024 // 16
+        else:  # 4 envs per CU: each may hold a quarter of the CU's LDS
+            assert L.lds_share == 160 * 1024 // 4 and L.lds_bytes <= L.lds_share
+    # at most one env per CU: the whole CU
+    cfg.num_envs = cus
+    assert lib.ssim_layout_for(ctypes.byref(cfg), ctypes.byref(L)) == 0
+    assert L.lds_resident == 1 and L.lds_share == 160 * 1024
     cfg.num_executors = 0
     assert lib.ssim_layout_for(ctypes.byref(cfg), ctypes.byref(L)) != 0
 
