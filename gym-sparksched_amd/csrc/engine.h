@@ -263,6 +263,12 @@ struct Sim {
   int32_t eid;    // env index
   bool res;       // hot block LDS-resident
   bool row_lds;   // observe()'s stage -> row map in the LDS scratch (else in the cold block; StateOffsets::row_of_lds)
+  // ex_lds (HBM-resident step / rollout launches): the executor records live in the wave's LDS scratch (sc_execs) for
+  // the launch — copied in by load_hot, back by save_hot — so their field reads (~40 per decision at N = 100) are LDS
+  // round trips instead of global loads queued behind the wave's earlier stores (vmcnt counts loads and stores in
+  // issue order), and their lines are not re-fetched from HBM every decision.
+  bool ex_l;
+  uint8_t* xb;    // ExecRec[0]: hot + O.execs, or the LDS copy
   EnvHeader h;    // register copy of the header
   Pcg64 rng;
   uint32_t iv_lane;  // Params::iv row `lane` (device: read with v_readlane instead of a scalar-cache load)
@@ -315,14 +321,16 @@ struct Sim {
   // row_cold: observe()'s stage -> row map in the cold block whatever the layout says (a kernel that gives the LDS the
   // layout left for it to something else: the persistent Decima rollout's policy plan).
   __device__ __forceinline__ Sim(const Params* __restrict__ p, uint8_t* state_arena, uint8_t* lds,
-                                 uint8_t* obs_arena, int32_t env_index, bool resident, bool row_cold = false)
+                                 uint8_t* obs_arena, int32_t env_index, bool resident, bool row_cold = false,
+                                 bool ex_lds = false)
       : L(p->L), D(p->D), C(p->C), IV(p->iv), NE(kN ? kN : p->L.num_executors), JC(kJ ? kJ : p->L.job_cap),
         SC(kS ? kS : p->L.stage_cap), O(state_offsets(NE, JC, SC)),
         ghot(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         hot(resident ? lds : state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes),
         cold(state_arena + kParamsReserve + (int64_t)env_index * O.env_bytes + O.hot_bytes),
         scr(resident ? lds + O.hot_bytes : lds), obs(obs_arena), eid(env_index), res(resident),
-        row_lds(resident || (!row_cold && W::uni(p->O.row_of_lds) != 0)) {
+        row_lds(resident || (!row_cold && W::uni(p->O.row_of_lds) != 0)), ex_l(ex_lds && !resident),
+        xb(ex_lds && !resident ? lds + O.sc_execs : hot + O.execs) {
     iv_lane = W::lane() < kIvRows ? *reinterpret_cast<const uint32_t*>(IV[W::lane()]) : 0u;
     dcache_on = kDurCache && W::uni(p->hp.dcache) != 0;
     HPp = &p->hp;
@@ -431,9 +439,10 @@ struct Sim {
       lo = W::min_i(b < lo ? b : lo);
     }
     for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
+      if (k0 >= h.commit_hw) break;
       const int k = k0 + W::lane();
       int b = kNone;
-      if (k < commit_cap_for(NE)) {
+      if (k < h.commit_hw) {
         const CommitRec r = cm(k);
         if (r.cnt > 0) {
           if (is_stage_pool(r.src)) b = pool_stage(r.src);
@@ -460,6 +469,7 @@ struct Sim {
                             list_span(O.sched_list, h.n_sched)};
       copy_spans(hot, ghot, live);
     }
+    if (ex_l) copy_execs(xb, ghot + O.execs);
     ev_regs_load();
     SSIM_TOC(t0, kPhLoadSave);
   }
@@ -473,7 +483,26 @@ struct Sim {
                              list_span(O.active_stages, h.n_active_stages), list_span(O.sched_list, h.n_sched)};
       copy_spans(ghot, hot, spans);
     }
+    if (ex_l) copy_execs(ghot + O.execs, xb);
     SSIM_TOC(t0, kPhLoadSave);
+  }
+  // ExecRec[N] between HBM and the LDS copy (ex_lds): 2N 16-B units, all loads of a lane issued before its stores
+  __device__ __forceinline__ void copy_execs(uint8_t* dst, const uint8_t* src) {
+    constexpr int kMax = (kN > 0 ? 2 * kN + W::kWidth - 1 : 2 * 256) / W::kWidth;  // (N <= 250: compute_layout)
+    const int n = 2 * NE;
+    u32x4 v[kMax];
+    W::sync();
+#pragma unroll
+    for (int u = 0; u < kMax; ++u) {
+      const int i = u * W::kWidth + W::lane();
+      if (i < n) v[u] = reinterpret_cast<const u32x4*>(src)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kMax; ++u) {
+      const int i = u * W::kWidth + W::lane();
+      if (i < n) reinterpret_cast<u32x4*>(dst)[i] = v[u];
+    }
+    W::sync();
   }
 
   // ---------------------------------------------------------------- field access
@@ -578,7 +607,7 @@ struct Sim {
   __device__ __forceinline__ StageRec& stage(int g) const { return H<StageRec>(O.stages)[g]; }
   __device__ __forceinline__ JobRec& job(int j) const { return H<JobRec>(O.jobs)[j]; }
   __device__ __forceinline__ JobTimes& jtimes(int j) const { return H<JobTimes>(O.jtimes)[j]; }
-  __device__ __forceinline__ ExecRec& exr(int e) const { return H<ExecRec>(O.execs)[e]; }
+  __device__ __forceinline__ ExecRec& exr(int e) const { return reinterpret_cast<ExecRec*>(xb)[e]; }
   __device__ __forceinline__ CommitRec& cm(int k) const { return H<CommitRec>(O.commits)[k]; }
   __device__ __forceinline__ PoolRec& pool(int p) const { return H<PoolRec>(O.pools)[p]; }
   __device__ __forceinline__ double* recent() const { return reinterpret_cast<double*>(cold + O.st_recent); }
@@ -657,9 +686,11 @@ struct Sim {
     if (src < 0) return;
     int hit = -1, freeslot = -1;
     SSIM_FIELD_STAT(13);
+    const int hw = h.commit_hw;
     for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
+      if (k0 >= hw) break;
       const int k = k0 + W::lane();
-      const bool ok = k < commit_cap_for(NE);
+      const bool ok = k < hw;
       CommitRec r{};
       if (ok) r = cm(k);
       const uint64_t mh = W::ballot(ok && r.cnt > 0 && r.src == src && r.dst == dst);
@@ -667,6 +698,9 @@ struct Sim {
       if (hit < 0 && mh) hit = k0 + W::ffs(mh);
       if (freeslot < 0 && mf) freeslot = k0 + W::ffs(mf);
     }
+    // slots >= commit_hw were never used this episode (cleared at reset): the first free slot of the whole array
+    if (freeslot < 0 && hw < commit_cap_for(NE)) freeslot = hw;
+    if (hit < 0 && freeslot >= hw) h.commit_hw = freeslot + 1;
     W::sync();
     if (hit >= 0) {
       if (W::lane() == 0) cm(hit).cnt = (int16_t)(cm(hit).cnt + n);
@@ -694,9 +728,10 @@ struct Sim {
   __device__ __forceinline__ int find_commit(int src, int dst) {
     SSIM_FIELD_STAT(13);
     for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
+      if (k0 >= h.commit_hw) break;
       const int k = k0 + W::lane();
       bool hit = false;
-      if (k < commit_cap_for(NE)) {
+      if (k < h.commit_hw) {
         const CommitRec r = cm(k);
         hit = r.cnt > 0 && r.src == src && r.dst == dst;
       }
@@ -736,9 +771,10 @@ struct Sim {
     int best_ord = 0x7FFFFFFF, best_dst = kPoolNone;
     SSIM_FIELD_STAT(13);
     for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
+      if (k0 >= h.commit_hw) break;
       const int k = k0 + W::lane();
       int ord = 0x7FFFFFFF, dst = kPoolNone;
-      if (k < commit_cap_for(NE)) {
+      if (k < h.commit_hw) {
         const CommitRec r = cm(k);
         if (r.cnt > 0 && r.src == p) {
           ord = r.ord;
@@ -761,9 +797,10 @@ struct Sim {
       int ord = 0x7FFFFFFF, k_best = -1;
       SSIM_FIELD_STAT(13);
       for (int k0 = 0; k0 < commit_cap_for(NE); k0 += W::kWidth) {
+        if (k0 >= h.commit_hw) break;
         const int k = k0 + W::lane();
         int o = 0x7FFFFFFF, kk = -1;
-        if (k < commit_cap_for(NE)) {
+        if (k < h.commit_hw) {
           const CommitRec r = cm(k);
           if (r.cnt > 0 && r.src == src && r.ord > last) {
             o = r.ord;

@@ -80,7 +80,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_e
                                              const int32_t* __restrict__ num_exec) {
   const int eid = blockIdx.x;
   if (env_idle(P, state, eid)) return;
-  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes);
+  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes, false, /*ex_lds=*/!kRes);
   StepIn a;
   a.stage_idx = stage_idx[eid];
   a.num_exec = num_exec[eid];
@@ -132,7 +132,7 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
 #ifdef SSIM_PROFILE
   const uint64_t rt_entry = WaveHip::realtime();
 #endif
-  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes, row_cold);
+  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes, row_cold, /*ex_lds=*/!kRes);
 #ifdef SSIM_PROFILE
   s.prof_set(kTCtor, WaveHip::realtime());
 #endif

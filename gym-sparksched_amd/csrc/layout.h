@@ -46,7 +46,7 @@ struct EnvHeader {
   int32_t step_events;
   int32_t src_idx;        // obs source_job_idx at the last observation
   int32_t err_line;       // engine.h line of the check that raised the first sticky error (diagnostic)
-  int32_t pad;
+  int32_t commit_hw;      // commitment slots used this episode: every live CommitRec has index < commit_hw
 };
 static_assert(sizeof(EnvHeader) % 16 == 0, "header must keep 16-B alignment");
 
@@ -157,7 +157,7 @@ struct StateOffsets {
   int64_t hdr, acc, jobs, jtimes, active_jobs, execs, sel_list, commits, stages, pools, active_stages,
       sched_list;
   int64_t st_recent /*cold f64[S]*/, pool_tab /*cold uint8 [P][set_cap]*/, row_of /*cold int16[S]*/;
-  int64_t sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
+  int64_t sc_execs /*ExecRec[N], HBM-resident step / rollout kernels (Sim ex_lds)*/, sc_keys_a, sc_keys_b /*int32[N+1]*/, sc_plan /*int32[2C]*/, sc_tab_a, sc_tab_b, sc_tab_p /*uint8[set_cap]*/,
       sc_dcache /*uint32[N][24] when N <= kDurCacheMaxExecs*/, sc_bits /*uint32[4]*/, sc_prof /*uint64[64], diagnostic -DSSIM_PROFILE build
       only*/, sc_row_of /*int16[S], last: LDS-resident kernels only*/;
   int64_t scratch_hbm_bytes;  // the scratch without sc_row_of: what an HBM-resident kernel allocates
@@ -222,6 +222,8 @@ constexpr StateOffsets state_offsets(int64_t N, int64_t J, int64_t S) {
   O.env_bytes = O.hot_bytes + O.cold_bytes;
 
   int64_t s = 0;
+  O.sc_execs = s;  // ExecRec[N]: the HBM-resident kernels' LDS copy of the executor records for a launch (Sim ex_lds)
+  s = align16(s + (int64_t)sizeof(ExecRec) * N);
   O.sc_keys_a = s;
   s = align16(s + 4 * (N + 1));
   O.sc_keys_b = s;

@@ -601,7 +601,8 @@ static DecimaLdsPlan decima_lds_plan(const Params& P) {
 #else
   const bool overlay = !O.lds_resident && L.num_executors > kDurCacheMaxExecs;
 #endif
-  const int64_t off = overlay ? 0 : align16(O.lds_resident ? O.scratch_bytes : O.scratch_hbm_bytes);
+  // (past the LDS copy of the executor records, sc_execs, which the HBM-resident engine keeps for the whole launch)
+  const int64_t off = overlay ? O.sc_keys_a : align16(O.lds_resident ? O.scratch_bytes : O.scratch_hbm_bytes);
   const int64_t base = O.lds_resident ? O.hot_bytes : 0;  // (the plan offset is relative to the scratch block)
   const int64_t room = O.lds_share - base - off;
   int cap = 0;

@@ -161,7 +161,8 @@ int hs_reset(hs_handle* h) {
 int hs_step(hs_handle* h, const int32_t* stage_idx, const int32_t* num_exec) {
   const Params* P = h->params;
   for (int e = 0; e < P->L.num_envs; ++e) {
-    Sim<WaveSerial> s(P, h->state, h->resident ? resident_lds(h) : h->scratch, h->obs, e, h->resident != 0);
+    Sim<WaveSerial> s(P, h->state, h->resident ? resident_lds(h) : h->scratch, h->obs, e, h->resident != 0, false,
+                      /*ex_lds=*/h->resident == 0);  // (the device's HBM-resident launches: executor records in LDS)
     StepIn a;
     a.stage_idx = stage_idx[e];
     a.num_exec = num_exec[e];
@@ -214,7 +215,8 @@ int hs_rollout_steps(hs_handle* h, int kind, uint64_t seed, const int32_t* env_s
   const Params* P = h->params;
   const int B = P->L.num_envs;
   for (int e = 0; e < B; ++e) {
-    Sim<WaveSerial> s(P, h->state, h->resident ? resident_lds(h) : h->scratch, h->obs, e, h->resident != 0);
+    Sim<WaveSerial> s(P, h->state, h->resident ? resident_lds(h) : h->scratch, h->obs, e, h->resident != 0, false,
+                      /*ex_lds=*/h->resident == 0);  // (the device's HBM-resident launches: executor records in LDS)
     PolicyView<WaveSerial> v{P->L, h->obs, e};
     const int steps = env_steps != nullptr && env_steps[e] < num_steps ? env_steps[e] : num_steps;
     s.load_hot();
