@@ -116,9 +116,10 @@ def test_layout_structs_match_header():
     # the bench shape (BASELINE configs[1]) runs its 1024 single-wave workgroups one per SIMD: four envs' LDS (hot
     # block + scratch) must fit a CU's 160 KB, or a quarter of the batch waits for a second round
     assert L.lds_resident == 1 and 4 * L.lds_bytes <= 160 * 1024, L.lds_bytes
-    # HBM-resident shapes run 4 one-wave workgroups per SIMD: 16 per CU must share its LDS. configs[3]'s shard
-    # (J=200, N=100) only fits with the stage->row map in the cold block; configs[2]'s (N=50) fits with it in LDS.
-    for n_exec, row_map_in_lds in ((100, False), (50, True)):
+    # HBM-resident shapes run 4 one-wave workgroups per SIMD: 16 per CU must share its LDS. With the LDS copy of the
+    # executor records (sc_execs, 32 B per executor) neither J=200 shard fits the stage->row map too: configs[3]'s
+    # (N=100) and configs[2]'s (N=50) keep it in the cold block.
+    for n_exec, row_map_in_lds in ((100, False), (50, False)):
         big = SsimConfig(num_envs=4096, num_executors=n_exec, job_cap=200, max_stages=18, max_edges=20,
                          moving_delay=2000.0, warmup_delay=1000.0, beta=0.0)
         assert lib.ssim_layout_for(ctypes.byref(big), ctypes.byref(L)) == 0
