@@ -22,6 +22,10 @@ def lib() -> ct.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # torch first: its HIP runtime must be the process's (the library's libamdhip64 dependency then resolves to the copy
+    # torch loaded). Loaded the other way round, torch's device init later fails ("no ROCm-capable device").
+    import torch  # noqa: F401
+
     if not os.path.exists(LIB_PATH):
         raise NativeError(
             f"libsparksched.so not found at {LIB_PATH}; build it with `python __graft_entry__.py build` "
