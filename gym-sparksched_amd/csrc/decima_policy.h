@@ -177,15 +177,21 @@ __host__ __device__ inline int dp_pack_src(int f) {
 
 // Weight sources: the packed copy in global memory, or its LDS copy (the persistent rollout's workgroups stage it).
 // grp(o): this lane's 16-B word of the group at o (16-B units); vec(o): the word at o (bias / last-layer vectors).
+// `lane`: this lane's index, made opaque per MLP call (dp_opaque): the per-lane word offsets (lane + a compile-time
+// offset, one per tile and group) and the lane-quarter conditions derived from it are then computed inside each call.
+// From a plain __lane_id() the compiler hoisted all of them to the kernel entry, where hundreds of such values were
+// live at once and went to scratch memory (the persistent rollout reloaded them from there in every MLP).
 struct DpWGlobal {
   const dp_f32x4* p;
-  __device__ __forceinline__ dp_f32x4 grp(int o) const { return p[o + (int)__lane_id()]; }
+  int lane = (int)__lane_id();
+  __device__ __forceinline__ dp_f32x4 grp(int o) const { return p[o + lane]; }
   __device__ __forceinline__ dp_f32x4 vec(int o) const { return p[o]; }
 };
 typedef __attribute__((address_space(3))) const dp_f32x4 dp_lds_f32x4;
 struct DpWLds {
   dp_lds_f32x4* p;
-  __device__ __forceinline__ dp_f32x4 grp(int o) const { return p[o + (int)__lane_id()]; }
+  int lane = (int)__lane_id();
+  __device__ __forceinline__ dp_f32x4 grp(int o) const { return p[o + lane]; }
   __device__ __forceinline__ dp_f32x4 vec(int o) const { return p[o]; }
 };
 // The weight pointer made opaque at each MLP call: every load derived from it is then loop-variant, so the compiler
@@ -196,11 +202,20 @@ __device__ __forceinline__ int64_t dp_zero() {  // an opaque 0 (offsets keep a p
   asm volatile("" : "+s"(z));
   return z;
 }
+__device__ __forceinline__ int dp_lane_opq() {  // __lane_id() behind an empty asm (not hoisted out of the caller)
+  int l = (int)__lane_id();
+  asm volatile("" : "+v"(l));
+  return l;
+}
 __device__ __forceinline__ DpWGlobal dp_opaque(DpWGlobal w) {
   w.p += dp_zero();
+  w.lane = dp_lane_opq();
   return w;
 }
-__device__ __forceinline__ DpWLds dp_opaque(DpWLds w) { return w; }
+__device__ __forceinline__ DpWLds dp_opaque(DpWLds w) {
+  w.lane = dp_lane_opq();
+  return w;
+}
 // A row-source pointer made opaque at each tile: the per-lane addresses of a tile's inputs (one per MFMA step) then
 // depend on the tile and are not hoisted out of the tile loops, where they were all live at once (64-bit addresses and
 // exec masks per step: the policy spilled to scratch memory even as a standalone kernel).
@@ -231,7 +246,7 @@ template <int IN, int H, class WS, class XF>
 __device__ __forceinline__ void dp_layer_in(const WS& w, int ow, int ob, XF xin, dp_f32x4 (&y)[H / 16]) {
   static_assert(H % 16 == 0, "layer widths: multiples of 16");
   constexpr int T = H / 16, STEPS = (IN + 3) / 4, G = (IN + 15) / 16;
-  const int q = (int)__lane_id() >> 4;
+  const int q = w.lane >> 4;
 #pragma unroll
   for (int t = 0; t < T; ++t) y[t] = w.vec(ob + 4 * t + q);
 #pragma unroll
@@ -258,7 +273,7 @@ __device__ __forceinline__ void dp_layer_h(const WS& w, int ow, int ob, const dp
                                            dp_f32x4 (&y)[H / 16]) {
   static_assert(H % 16 == 0 && HP % 16 == 0, "layer widths: multiples of 16");
   constexpr int T = H / 16, TP = HP / 16;
-  const int q = (int)__lane_id() >> 4;
+  const int q = w.lane >> 4;
 #pragma unroll
   for (int t = 0; t < T; ++t) y[t] = w.vec(ob + 4 * t + q);
 #pragma unroll
@@ -294,7 +309,7 @@ __device__ __forceinline__ float dp_mlp1(const WS& w0, int pb, XF xin) {
   dp_f32x4 a1[H1 / 16], a2[H2 / 16];
   dp_layer_in<IN, H1>(w, pb + PL::kW0, pb + PL::kB0, xin, a1);
   dp_layer_h<H1, H2, true>(w, pb + PL::kW1, pb + PL::kB1, a1, a2);
-  const int q = (int)__lane_id() >> 4;
+  const int q = w.lane >> 4;
   float part = q == 0 ? w.vec(pb + PL::kB2)[0] : 0.0f;  // the last layer (H2 -> 1) on the VALU: this quarter's units,
 #pragma unroll                                          // then all four
   for (int t = 0; t < H2 / 16; ++t) {

@@ -5,7 +5,19 @@
 
 struct WaveHip {
   static constexpr int kWidth = 64;
+  // SSIM_OPAQUE_LANE (set per translation unit, for the 4-wave HBM-resident kernels): the lane index behind an empty
+  // asm at every use. From a plain __lane_id() the compiler hoists every per-lane address and lane condition derived
+  // from it (base + lane x stride, for dozens of arrays) to the kernel entry, where at the 128-VGPR cap they are spilled
+  // to scratch memory and reloaded at each use; opaque, each is recomputed (a VALU op or two) where it is used.
+#if SSIM_OPAQUE_LANE
+  __device__ static __forceinline__ int lane() {
+    int l = (int)__lane_id();
+    asm volatile("" : "+v"(l));
+    return l;
+  }
+#else
   __device__ static __forceinline__ int lane() { return (int)__lane_id(); }
+#endif
   __device__ static __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
   __device__ static __forceinline__ int ffs(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
   __device__ static __forceinline__ int popc(uint64_t m) { return __popcll((unsigned long long)m); }
