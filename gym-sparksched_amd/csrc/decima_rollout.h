@@ -21,6 +21,14 @@
 #include "decima.h"
 #include "decima_policy.h"
 
+// 1: the HBM-resident Decima rollout keeps the executor records in LDS for the launch (Sim ex_lds), after which the
+// policy plan starts (sparksched.hip decima_lds_plan); 0 (default): in HBM, and the plan takes the wave's whole LDS share
+// from the scratch's start. The larger plan keeps more observations off the global plan: measured 2.82e7 vs 2.77e7
+// decisions/s, HBM writes 5.8 vs 8.0 KB per decision (profiles/r06/decima_ex_lds/).
+#ifndef SSIM_DR_EX_LDS
+#define SSIM_DR_EX_LDS 0
+#endif
+
 // Per-env global workspace: [features scratch (decima.h) | policy plan for stage_cap nodes (decima_policy.h)], then
 // the feature outputs for all envs (the ssim_decima_features layout).
 struct DecimaWork {
@@ -297,7 +305,7 @@ __device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P
   a.test_reject = (flags & SSIM_ROLLOUT_TEST_REJECT) != 0;
   const DecimaPolicy pol{P, obs, a};
   rollout_body<kRes, kN, kJ, 0, DecimaPolicy>(P, state, obs, pol, num_steps, flags, limits, reset, action_log, prof_out,
-                                              budget, nullptr, !kRes);
+                                              budget, nullptr, !kRes, SSIM_DR_EX_LDS != 0);
 }
 #define SSIM_DR_WAVES(kRes) ((kRes) ? 1 : SSIM_DECIMA_ROLLOUT_WAVES)
 template <bool kRes, int kN = 0, int kJ = 0>

@@ -102,7 +102,8 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
                                                 const Pol& pol, int num_steps, int flags,
                                                 const double* __restrict__ limits, uint8_t* reset,
                                                 int32_t* action_log, uint64_t* prof_out, int64_t budget,
-                                                const int32_t* __restrict__ env_steps, bool row_cold = false) {
+                                                const int32_t* __restrict__ env_steps, bool row_cold = false,
+                                                bool ex_lds = true) {
   const int eid = blockIdx.x;
   const int B = P->L.num_envs;
   if (budget > 0 && eid == 0 && WaveHip::lane() <= kStopLines)  // the next budget launch's slot (TicketStop)
@@ -132,7 +133,7 @@ __device__ __forceinline__ void rollout_body(const Params* __restrict__ P, uint8
 #ifdef SSIM_PROFILE
   const uint64_t rt_entry = WaveHip::realtime();
 #endif
-  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes, row_cold, /*ex_lds=*/!kRes);
+  Sim<WaveHip, kN, kJ, kS> s(P, state, g_smem, obs, eid, kRes, row_cold, ex_lds && !kRes);
 #ifdef SSIM_PROFILE
   s.prof_set(kTCtor, WaveHip::realtime());
 #endif

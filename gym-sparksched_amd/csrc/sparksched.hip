@@ -594,15 +594,19 @@ static DecimaLdsPlan decima_lds_plan(const Params& P) {
   const ssim_layout& L = P.L;
   DecimaLdsPlan pl{0, 0, O.lds_bytes};
   const int64_t eng = O.lds_resident ? O.hot_bytes + O.scratch_bytes : O.scratch_hbm_bytes;  // (HBM: row map cold)
-  // HBM-resident engines without the duration-descriptor cache hold only per-operation temporaries in their LDS
-  // scratch (set tables, key lists, the commitment plan), none live across a decision: the plan overlays them.
+  // Engines without the duration-descriptor cache hold only per-operation temporaries in their LDS scratch (set
+  // tables, key lists, the commitment plan, observe()'s stage -> row map), none live across a decision: the plan
+  // overlays them. (Round 6: LDS-resident engines too — the PPO collect's J = 200 / N = 50 envs keep a 146 KB hot block
+  // in a CU's 160 KB, and overlaying their 10.8 KB scratch takes the plan from ~8 to ~60 nodes, so nearly every
+  // decision's policy runs from LDS instead of the global plan.)
 #ifdef SSIM_PROFILE
   const bool overlay = false;  // (the profile sums live in the scratch)
 #else
-  const bool overlay = !O.lds_resident && L.num_executors > kDurCacheMaxExecs;
+  const bool overlay = L.num_executors > kDurCacheMaxExecs;
 #endif
-  // (past the LDS copy of the executor records, sc_execs, which the HBM-resident engine keeps for the whole launch)
-  const int64_t off = overlay ? O.sc_keys_a : align16(O.lds_resident ? O.scratch_bytes : O.scratch_hbm_bytes);
+  // (past the LDS copy of the executor records, sc_execs, when the HBM-resident engine keeps one for the launch)
+  const int64_t off = overlay ? (!O.lds_resident && SSIM_DR_EX_LDS ? O.sc_keys_a : 0)
+                              : align16(O.lds_resident ? O.scratch_bytes : O.scratch_hbm_bytes);
   const int64_t base = O.lds_resident ? O.hot_bytes : 0;  // (the plan offset is relative to the scratch block)
   const int64_t room = O.lds_share - base - off;
   int cap = 0;

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/ab_decima_pmc
 mkdir -p "$OUT"
 ARGS="--workload decima --steps 40 --warmup 5 --no-cpu-baseline"
-for lib in gym-sparksched_amd/build/ab/*.so; do
+for lib in gym-sparksched_amd/build/${AB_OUT:-ab}/*.so; do
   n=$(basename "$lib" .so)
   SSIM_LIB="$PWD/$lib" timeout -k 10 300 python bench.py $ARGS > "$OUT/${n}_bench.log" 2>&1
   rc=$?; echo "$n bench rc=$rc $(grep -o '"value": [0-9.]*' $OUT/${n}_bench.log)"
