@@ -317,8 +317,8 @@ __device__ __forceinline__ float dp_mlp1(const WS& w0, int pb, XF xin) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) part = __builtin_fmaf(w2[r], dp_tanh(a2[t][r]), part);
   }
-  part += __shfl_xor(part, 16);
-  return part + __shfl_xor(part, 32);
+  part += WaveHip::shfl_xor_f(part, 16);
+  return part + WaveHip::shfl_xor_f(part, 32);
 }
 
 // Gumbel(0,1) noise from a counter-based stream (splitmix64 of seed, env, counter, item).

@@ -78,12 +78,28 @@ struct WaveHip {
   __device__ static __forceinline__ void lds_add_u64(uint64_t* p, uint64_t v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
+  // Cross-lane reads through ds_bpermute with the source lane computed from lane() (opaque in the 4-wave units): HIP's
+  // __shfl_xor / __shfl_up compute it from their own __lane_id(), and the compiler hoisted those per-lane addresses
+  // (six per butterfly) to the kernel entry and spilled them.
+  __device__ static __forceinline__ int shfl_xor_i(int v, int off) {
+    return __builtin_amdgcn_ds_bpermute((lane() ^ off) << 2, v);
+  }
+  __device__ static __forceinline__ float shfl_xor_f(float v, int off) {
+    return __builtin_bit_cast(float, shfl_xor_i(__builtin_bit_cast(int, v), off));
+  }
+  __device__ static __forceinline__ double shfl_xor_d(double v, int off) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int a = (lane() ^ off) << 2;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)b);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+  }
   __device__ static __forceinline__ int excl_scan(int x, int* total) {
     int v = x;
     const int l = lane();
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(v, (unsigned)off);
+      const int y = __builtin_amdgcn_ds_bpermute(((l - off) & 63) << 2, v);  // (used only where l >= off)
       if (l >= off) v += y;
     }
     *total = __builtin_amdgcn_readlane(v, 63);  // SGPR: the running total stays wave-uniform
@@ -91,7 +107,7 @@ struct WaveHip {
   }
   __device__ static __forceinline__ double sum_d(double x) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    for (int off = 32; off > 0; off >>= 1) x += shfl_xor_d(x, off);
     return uni(x);
   }
   // Sparse argmins: the candidates are few (live commitments, pending executor events), so walk the
@@ -210,20 +226,20 @@ struct WaveHip {
   __device__ static __forceinline__ float max_f(float x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-      const float y = __shfl_xor(x, off);
+      const float y = shfl_xor_f(x, off);
       x = y > x ? y : x;
     }
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
   }
   __device__ static __forceinline__ float sum_f(float x) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    for (int off = 32; off > 0; off >>= 1) x += shfl_xor_f(x, off);
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
   }
   __device__ static __forceinline__ int min_i(int x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-      const int y = __shfl_xor(x, off);
+      const int y = shfl_xor_i(x, off);
       x = y < x ? y : x;
     }
     return uni(x);
@@ -231,7 +247,7 @@ struct WaveHip {
   __device__ static __forceinline__ int max_i(int x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-      const int y = __shfl_xor(x, off);
+      const int y = shfl_xor_i(x, off);
       x = y > x ? y : x;
     }
     return uni(x);
