@@ -177,3 +177,26 @@ def test_bench_decima_timed_steps_replay(gpu_device, dataset):
     res = cases.replay_many(DECIMA, dataset, [(seeds[i], lim[i], actions[i]) for i in sample])
     for i, (o, ob, ep, dec, last) in zip(sample, res):
         cases.check_replayed_env(eng, v, ta, tc, i, o, ob, ep, dec, last, "decima-bench")
+
+
+@pytest.mark.parametrize("n_exec,jobs,B,seed0", [(3, 20, 3, 31), (16, 30, 2, 41), (127, 20, 1, 51)])
+def test_forced_hbm_generic_kernel_lockstep(make, dataset, n_exec, jobs, B, seed0):
+    """Shapes without a specialised unit on the generic HBM-resident kernels (`hbm`: run-time executor count, the
+    executor records' LDS copy sized at run time, the opaque lane index): full-episode lockstep with random actions, every
+    5th observation, the event trace and the job times vs the oracle. N = 16 and 127 take the paged set tables."""
+    import parity
+    from oracle.policies import RandomPolicy
+    from oracle.restatement import SparkSchedOracle
+    from spark_sched_sim import native
+
+    cfg = dict(TPCH, num_executors=n_exec, job_arrival_cap=jobs)
+    eng = make(cfg, B, dataset, 100000, config_flags=_abi.SSIM_CFG_FORCE_HBM)
+    assert int(eng.layout.lds_resident) == 0
+    assert native.lib().ssim_debug_kernel_name(eng.handle, 0).decode() == "hbm"
+    oracles = [SparkSchedOracle(cfg, dataset) for _ in range(B)]
+    steps = parity.run_lockstep(eng, oracles, seeds=[seed0 + i for i in range(B)],
+                                policy_factory=lambda i: RandomPolicy(42 + i), check_every=5)
+    assert min(steps) > 20
+    parity.compare_traces(eng, oracles)
+    ta, tc, _ = eng.job_times_np()
+    parity.compare_job_times(ta, tc, oracles)
