@@ -2154,10 +2154,13 @@ struct Sim {
   // when the queue ran dry (or the env froze), kSimPreempted when `stop` fired between two events (the state is
   // then exactly the reference's between those events; a later call continues the loop).
   // The stop condition is a read of one shared word (TicketStop): polled every kStopEvery-th event, issued one
-  // event before it is tested so its latency hides behind that event. Most steps take fewer events and finish
-  // unpolled; the long ones (hundreds of task events) are the launch tail preemption removes.
+  // event before it is tested so its latency hides behind that event. A launch ends when its last wave has seen the
+  // flag, so the poll interval is the launch's tail. Round 6 (50 timed 20-step launches per run, low-noise,
+  // `profiles/r06/ab_stop_poll/`): every event 3.21·10⁷ vs every 8th 3.12·10⁷ decisions/s on the driver's window,
+  // +0.9% at 300 steps, +1.1% on configs[3], configs[2] within noise (round 2's and 5's single-window A/Bs could not
+  // resolve it).
 #ifndef SSIM_STOP_EVERY
-#define SSIM_STOP_EVERY 8
+#define SSIM_STOP_EVERY 1
 #endif
   static constexpr int kStopEvery = SSIM_STOP_EVERY;  // a power of two
   template <class Stop>
