@@ -290,6 +290,78 @@ __device__ __forceinline__ void dp_layer_h(const WS& w, int ow, int ob, const dp
     __builtin_amdgcn_sched_barrier(0);
   }
 }
+// SSIM_DP_PIPELINE (set by the one-wave-per-SIMD translation units, k_dr_lds*.hip): the same layers with every weight
+// and input load issued one group ahead of the steps that use it, and each MLP's biases, first weight group of every
+// layer and last-layer vector loaded at its start, so one MLP waits for one round of loads instead of one per group
+// (~8 for a score MLP: at one wave per SIMD nothing else hides them). The same operands in the same order: the results
+// are those of the plain layers bit for bit. (~100 more registers in flight: the 4-wave units, at 128, keep the plain
+// form.)
+#ifndef SSIM_DP_PIPELINE
+#define SSIM_DP_PIPELINE 0
+#endif
+#if SSIM_DP_PIPELINE
+// first layer with its group 0 weights in wa and its biases in y already
+template <int IN, int H, class WS, class XF>
+__device__ __forceinline__ void dp_layer_in_p(const WS& w, int ow, XF xin, dp_f32x4 (&wa)[H / 16],
+                                              dp_f32x4 (&y)[H / 16]) {
+  constexpr int T = H / 16, STEPS = (IN + 3) / 4, G = (IN + 15) / 16;
+  const int q = w.lane >> 4;
+  auto in = [&](int st) { return st < STEPS && (4 * st + 3 < IN || 4 * st + q < IN) ? xin(4 * st + q) : 0.0f; };
+  float xa[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) xa[j] = in(j);
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    dp_f32x4 wn[T];
+    float xn[4];
+    if (g + 1 < G) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) wn[t] = w.grp(ow + (t * G + g + 1) * 64);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xn[j] = in(4 * (g + 1) + j);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (4 * g + j < STEPS) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][j], xa[j], y[t], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + 1 < G) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) wa[t] = wn[t];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xa[j] = xn[j];
+    }
+  }
+}
+// hidden / output layer with its group 0 weights in wa and its biases in y already
+template <int HP, int H, bool kTanh, class WS>
+__device__ __forceinline__ void dp_layer_h_p(const WS& w, int ow, const dp_f32x4 (&x)[HP / 16],
+                                             dp_f32x4 (&wa)[H / 16], dp_f32x4 (&y)[H / 16]) {
+  constexpr int T = H / 16, TP = HP / 16;
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp) {
+    dp_f32x4 wn[T];
+    if (tp + 1 < TP) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) wn[t] = w.grp(ow + (t * TP + tp + 1) * 64);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float xv = dp_act<kTanh>(x[tp][r]);
+#pragma unroll
+      for (int t = 0; t < T; ++t) y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][r], xv, y[t], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (tp + 1 < TP) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) wa[t] = wn[t];
+    }
+  }
+}
+#endif
 // 3-layer MLP with 16 outputs (the GNN MLPs, LeakyReLU(0.2) between layers) at packed base `pb`: y register r of lane
 // l = output 4 (l >> 4) + r of row l & 15
 template <int IN, int H1, int H2, class WS, class XF>
@@ -297,9 +369,30 @@ __device__ __forceinline__ void dp_mlp16(const WS& w0, int pb, XF xin, dp_f32x4 
   using PL = Mlp3P<IN, H1, H2, kDpEmb>;
   const WS w = dp_opaque(w0);
   dp_f32x4 a1[H1 / 16], a2[H2 / 16];
+#if SSIM_DP_PIPELINE
+  constexpr int T1 = H1 / 16, T2 = H2 / 16;
+  const int q = w.lane >> 4;
+  dp_f32x4 w0g[T1], w1g[T2], w2g[1];
+#pragma unroll
+  for (int t = 0; t < T1; ++t) {
+    a1[t] = w.vec(pb + PL::kB0 + 4 * t + q);
+    w0g[t] = w.grp(pb + PL::kW0 + t * PL::G0 * 64);
+  }
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    a2[t] = w.vec(pb + PL::kB1 + 4 * t + q);
+    w1g[t] = w.grp(pb + PL::kW1 + t * T1 * 64);
+  }
+  y[0] = w.vec(pb + PL::kB2 + q);
+  w2g[0] = w.grp(pb + PL::kW2);
+  dp_layer_in_p<IN, H1>(w, pb + PL::kW0, xin, w0g, a1);
+  dp_layer_h_p<H1, H2, false>(w, pb + PL::kW1, a1, w1g, a2);
+  dp_layer_h_p<H2, kDpEmb, false>(w, pb + PL::kW2, a2, w2g, y);
+#else
   dp_layer_in<IN, H1>(w, pb + PL::kW0, pb + PL::kB0, xin, a1);
   dp_layer_h<H1, H2, false>(w, pb + PL::kW1, pb + PL::kB1, a1, a2);
   dp_layer_h<H2, kDpEmb, false>(w, pb + PL::kW2, pb + PL::kB2, a2, y);
+#endif
 }
 // 3-layer MLP with one output (the policy score MLPs, Tanh between layers): the score of row l & 15, in every quarter
 template <int IN, int H1, int H2, class WS, class XF>
@@ -307,9 +400,32 @@ __device__ __forceinline__ float dp_mlp1(const WS& w0, int pb, XF xin) {
   using PL = Mlp3P<IN, H1, H2, 1>;
   const WS w = dp_opaque(w0);
   dp_f32x4 a1[H1 / 16], a2[H2 / 16];
+  const int q = w.lane >> 4;
+#if SSIM_DP_PIPELINE
+  constexpr int T1 = H1 / 16, T2 = H2 / 16;
+  dp_f32x4 w0g[T1], w1g[T2], w2v[T2];
+#pragma unroll
+  for (int t = 0; t < T1; ++t) {
+    a1[t] = w.vec(pb + PL::kB0 + 4 * t + q);
+    w0g[t] = w.grp(pb + PL::kW0 + t * PL::G0 * 64);
+  }
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    a2[t] = w.vec(pb + PL::kB1 + 4 * t + q);
+    w1g[t] = w.grp(pb + PL::kW1 + t * T1 * 64);
+    w2v[t] = w.vec(pb + PL::kW2 + 4 * t + q);
+  }
+  float part = q == 0 ? w.vec(pb + PL::kB2)[0] : 0.0f;
+  dp_layer_in_p<IN, H1>(w, pb + PL::kW0, xin, w0g, a1);
+  dp_layer_h_p<H1, H2, true>(w, pb + PL::kW1, a1, w1g, a2);
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part = __builtin_fmaf(w2v[t][r], dp_tanh(a2[t][r]), part);
+  }
+#else
   dp_layer_in<IN, H1>(w, pb + PL::kW0, pb + PL::kB0, xin, a1);
   dp_layer_h<H1, H2, true>(w, pb + PL::kW1, pb + PL::kB1, a1, a2);
-  const int q = w.lane >> 4;
   float part = q == 0 ? w.vec(pb + PL::kB2)[0] : 0.0f;  // the last layer (H2 -> 1) on the VALU: this quarter's units,
 #pragma unroll                                          // then all four
   for (int t = 0; t < H2 / 16; ++t) {
@@ -317,6 +433,7 @@ __device__ __forceinline__ float dp_mlp1(const WS& w0, int pb, XF xin) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) part = __builtin_fmaf(w2[r], dp_tanh(a2[t][r]), part);
   }
+#endif
   part += WaveHip::shfl_xor_f(part, 16);
   return part + WaveHip::shfl_xor_f(part, 32);
 }
@@ -326,6 +443,73 @@ __device__ __forceinline__ float dp_gumbel(uint64_t key, uint64_t item) {
   const uint64_t r = splitmix64(key ^ splitmix64(item + 0x632BE59BD9B4E019ULL));
   const double u = ((double)(r >> 11) + 0.5) * (1.0 / 9007199254740992.0);  // (0, 1)
   return (float)(-log(-log(u)));
+}
+
+// Exec-score helpers (the one-env-per-CU persistent rollout, k_dr_lds50): the env's workgroup has kDpHelpWaves waves,
+// wave 0 runs the env and the others score exec-action tiles. The exec MLP (36 -> 64 -> 64 -> 1) is a ~10k-cycle chain
+// per 16-row tile on one SIMD. Two ways to take it off wave 0's chain, through the LDS mailbox below (the tiles' shared
+// inputs out, the scores back; two workgroup barriers per decision order it: published -> A -> tiles -> B -> read):
+// * speculative: when the schedulable nodes' DAGs (at most kDpSpecCand) need at most kDpHelpWaves - 1 tiles in all,
+//   the helpers score every candidate DAG's actions while wave 0 scores the stages, and wave 0 then reads the chosen
+//   DAG's (barrier A before the stage tiles, B after them);
+// * otherwise, after the stage draw, the chosen DAG's tiles over all the waves (tile j on wave j % kDpHelpWaves).
+// The same MLP, inputs and Gumbel noise as the one-wave loop of decima_policy_env, so the same values bit for bit.
+// The helpers' loop waits at barrier A and leaves on kDpHelpExit, which wave 0 publishes once its rollout ends
+// (decima_rollout.h).
+constexpr int kDpHelpWaves = 4;
+constexpr int kDpSpecCand = 3;
+enum : int32_t { kDpHelpWork = 1, kDpHelpExit = 2 };
+struct DpHelp {
+  int32_t cmd, ncand, first;  // kDpHelpWork / kDpHelpExit; candidate DAGs; the first wave taking tiles (1: helpers only)
+  int32_t cap[kDpSpecCand];   // exec actions to score (k < cap) per candidate
+  int32_t dag[kDpSpecCand];   // the candidates' DAGs
+  int32_t pad;
+  uint64_t key;               // the decision's Gumbel key
+  float base[kDpSpecCand][36];  // exec-MLP inputs 0..34 of every row of the candidate (input 35 is the row's k / N)
+};
+// mailbox bytes for N executors: the header, then sc [kDpSpecCand][N] and the Gumbel-perturbed scores gs [..][N]
+__host__ __device__ inline int64_t dp_help_bytes(int64_t n_exec) {
+  return align16((int64_t)sizeof(DpHelp) + 8 * kDpSpecCand * n_exec);
+}
+__device__ __forceinline__ float* dp_help_sc(DpHelp* hb, int N, int c) { return reinterpret_cast<float*>(hb + 1) + c * N; }
+__device__ __forceinline__ float* dp_help_gs(DpHelp* hb, int N, int c) {
+  return reinterpret_cast<float*>(hb + 1) + (kDpSpecCand + c) * N;
+}
+
+// The mailbox's tiles assigned to wave w: tile j (candidates in order, then rows) runs on wave first + j % (waves -
+// first); action k of candidate c: its score into sc[c][k], its Gumbel-perturbed score into gs[c][k].
+template <class WS>
+__device__ __forceinline__ void dp_exec_tiles(const WS& Wt, DpHelp* hb, int N, int w) {
+  using W = WaveHip;
+  const int nc = W::uni(hb->ncand), first = W::uni(hb->first);
+  const uint64_t key = W::uni(hb->key);
+  const int lane = W::lane(), rl = lane & 15, hl = lane >> 4;
+  int j = 0;
+  for (int c = 0; c < nc; ++c) {
+    const int cap = W::uni(hb->cap[c]);
+    for (int t0 = 0; t0 < cap; t0 += 16, ++j) {
+      if (first + j % (kDpHelpWaves - first) != w) continue;
+      const int k = t0 + rl;
+      const float* bq = dp_opq(hb->base[c]);
+      const float sc = dp_mlp1<3 + 2 * kDpEmb + 1, 64, 64>(Wt, kPExec, [&](int f) {
+        return f < 3 + 2 * kDpEmb ? bq[f] : (float)k / (float)N;
+      });
+      if (k < cap && hl == 0) {
+        dp_help_sc(hb, N, c)[k] = sc;
+        dp_help_gs(hb, N, c)[k] = sc + dp_gumbel(key ^ 0xE7037ED1A0B428DBULL, (uint64_t)k);
+      }
+    }
+  }
+}
+// The helper waves' loop (waves 1 .. kDpHelpWaves - 1 of a helped workgroup)
+template <class WS>
+__device__ __forceinline__ void dp_help_loop(const WS& Wt, DpHelp* hb, int N, int w) {
+  for (;;) {
+    __syncthreads();  // A: a decision's inputs published, or the exit
+    if (WaveHip::uni(hb->cmd) != kDpHelpWork) return;
+    dp_exec_tiles(Wt, hb, N, w);
+    __syncthreads();  // B: scores written
+  }
 }
 
 struct DecimaPolicyOut {
@@ -365,15 +549,16 @@ __device__ __forceinline__ float dp_ld(const float* p) {
 // Returns false if the env has more nodes than the plan holds (the caller reports it). `lds`: the plan, in LDS
 // (k_decima_policy) or, with kGlobal, a per-env region of global memory (the persistent Decima rollout, whose
 // 16 waves per CU leave no LDS for a J=200 plan); the atomic accumulation phases then end with an agent-scope
-// fence (decima.h scratch_sync). `act` (optional) receives the action.
-template <bool kGlobal = false, class WS>
+// fence (decima.h scratch_sync). `act` (optional) receives the action. kHelp: the exec scores run on the workgroup's
+// helper waves through the LDS mailbox `help` (dp_exec_tiles).
+template <bool kGlobal = false, bool kHelp = false, class WS>
 __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, const uint8_t* __restrict__ obs,
                                          const float* __restrict__ feats, const int32_t* __restrict__ ccap,
                                          const uint32_t* __restrict__ emask, const int32_t* __restrict__ depth,
                                          const WS& Wt, int node_cap, uint64_t seed,
                                          uint64_t counter, int eid, uint8_t* lds, const DecimaPolicyOut& o,
                                          DpAction* act = nullptr, uint64_t* prof = nullptr,
-                                         int dag_cap = 0) {
+                                         int dag_cap = 0, DpHelp* help = nullptr) {
   using W = WaveHip;
   // diagnostic -DSSIM_PROFILE builds: shader cycles per part and the observation's sizes into prof[0..9] (LDS, lane 0)
 #ifdef SSIM_PROFILE
@@ -390,6 +575,14 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   (void)prof;
   auto lap = [](int) {};
   auto count = [](int, uint64_t) {};
+#endif
+  // -DSSIM_PROFILE_FINE (with SSIM_PROFILE): slots 5..8 time the score sections' parts instead of counting sizes
+#ifdef SSIM_PROFILE_FINE
+  auto lapf = [&](int slot) { lap(slot); };
+  auto countf = [](int, uint64_t) {};
+#else
+  auto lapf = [](int) {};
+  auto countf = [&](int slot, uint64_t v) { count(slot, v); };
 #endif
   const ssim_layout& L = P->L;
   const int S = L.stage_cap, J = L.job_cap, E = L.edge_cap, N = L.num_executors;
@@ -451,9 +644,9 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   for (int e = lane; e < ne; e += 64) flag[(int)links[2 * e]] = 1;  // parent has a child
   scratch_sync<W, kGlobal>();
   lap(0);  // setup
-  count(5, (uint64_t)n);
-  count(6, (uint64_t)ne);
-  count(7, (uint64_t)levels);
+  countf(5, (uint64_t)n);
+  countf(6, (uint64_t)ne);
+  countf(7, (uint64_t)levels);
   // h_init = mlp_prep(x); h = h_init (no levels) or mlp_update(h_init) for leaves. Tiles of 16 nodes (every lane runs
   // the matrix-core MLPs: the tile loops are wave-uniform); lane l stores outputs 4 (l >> 4) + r, r < 4, of node
   // t0 + (l & 15).
@@ -595,6 +788,55 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
     nsch += W::popc(b);
   }
   scratch_sync<W, kGlobal>();
+  // exec-MLP inputs of DAG gc into mailbox slot c (kHelp)
+  auto publish = [&](int c, int gc, int capc, int pc) {
+    if (lane < 3 + 2 * kDpEmb)
+      help->base[c][lane] = lane < 3            ? x[pc * kDecimaFeatures + lane]
+                            : lane < 3 + kDpEmb ? dp_ld<kGlobal>(hdag + gc * kDpEmb + lane - 3)
+                                                : dp_ld<kGlobal>(glob + lane - 3 - kDpEmb);
+    if (lane == 0) {
+      help->cap[c] = capc;
+      help->dag[c] = gc;
+    }
+  };
+  bool spec = false;  // the candidates' exec scores on the helpers, during the stage tiles
+  if constexpr (kHelp) {
+    if (nsch <= 64) {
+      const int gl = lane < nsch ? ndag[slist[lane]] : -1;
+      const int cl = lane < nsch ? cc[gl] : 0, pl = lane < nsch ? ptr[gl] : 0;  // (one round trip for all)
+      int cg[kDpSpecCand], cc_[kDpSpecCand], cp[kDpSpecCand], nc = 0, tiles = 0;
+      for (int s = 0; s < nsch; ++s) {  // distinct DAGs in schedulable-node order
+        const int gs = W::bcast_i(gl, s);
+        bool seen = false;
+#pragma unroll
+        for (int c = 0; c < kDpSpecCand; ++c) seen |= c < nc && cg[c] == gs;
+        if (seen) continue;
+        if (nc == kDpSpecCand) {
+          nc = kDpSpecCand + 1;
+          break;
+        }
+        cg[nc] = gs;
+        cc_[nc] = min(max(W::bcast_i(cl, s), 0), N);
+        cp[nc] = W::bcast_i(pl, s);
+        tiles += (cc_[nc] + 15) / 16;
+        ++nc;
+      }
+      spec = nc <= kDpSpecCand && tiles > 0 && tiles < kDpHelpWaves;
+      if (spec) {
+#pragma unroll
+        for (int c = 0; c < kDpSpecCand; ++c)
+          if (c < nc) publish(c, cg[c], cc_[c], cp[c]);
+        if (lane == 0) {
+          help->ncand = nc;
+          help->first = 1;
+          help->key = key;
+          help->cmd = kDpHelpWork;
+        }
+        __syncthreads();  // A
+      }
+    }
+  }
+  lapf(5);  // (fine: stage compaction)
   float mx = -__builtin_inff(), best = -__builtin_inff();
   int pick = -1;
   for (int t0 = 0; t0 < nsch; t0 += 16) {  // score = mlp_stage([x, h, h_dag, h_glob]) per schedulable node
@@ -623,6 +865,10 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
       }
     }
   }
+  if constexpr (kHelp) {
+    if (spec) __syncthreads();  // B (before any return: the helpers meet it)
+  }
+  lapf(6);  // (fine: stage tiles)
   mx = W::max_f(mx);
   // winning lane of the Gumbel race (ties: lowest node)
   const float bmax = W::max_f(best);
@@ -648,15 +894,54 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
   z = W::sum_f(z);
   const float lp_stage = score[node] - mx - logf(z);
   lap(4);  // stage scores + draw
-  count(8, (uint64_t)nsch);
+  countf(8, (uint64_t)nsch);
   // exec scores for k < commit cap of the chosen DAG
   const int g = ndag[node];
   const int cap = min(max(W::uni(cc[g]), 0), N);
   const int p0 = ptr[g];
+  lapf(7);  // (fine: exec prologue)
   float emx = -__builtin_inff(), ebest = -__builtin_inff(), es_k = 0.0f;
   int epick = -1;
   float* escore = agg;  // [N] (agg is free after message passing)
-  for (int t0 = 0; t0 < cap; t0 += 16) {  // score of exec action k / N, k < cap, from [x_dag[:3], h_dag, h_glob, k/N]
+  if constexpr (kHelp) {  // the tiles over the workgroup's waves (dp_exec_tiles), then the same reduction
+    int c = 0;
+    if (spec) {  // already scored: the chosen DAG's slot
+      const int nc = W::uni(help->ncand);
+      for (int c2 = 1; c2 < nc; ++c2)
+        if (W::uni(help->dag[c2]) == g) c = c2;
+    }
+    if (!spec) {
+      publish(0, g, cap, p0);
+      if (lane == 0) {
+        help->ncand = 1;
+        help->first = 0;
+        help->key = key;
+        help->cmd = kDpHelpWork;
+      }
+      const bool many = cap > 16;  // one tile: no helpers needed
+      if (many) __syncthreads();  // A
+      else W::sync();
+      dp_exec_tiles(Wt, help, N, 0);
+      if (many) __syncthreads();  // B
+      else W::sync();
+    }
+    escore = dp_help_sc(help, N, c);
+    const float* egs = dp_help_gs(help, N, c);
+    for (int t0 = 0; t0 < cap; t0 += 16) {
+      const int k = t0 + rl;
+      if (k < cap && hl == 0) {
+        const float sc = escore[k], gs = egs[k];
+        if (o.exec_scores) o.exec_scores[(int64_t)eid * N + k] = sc;
+        emx = sc > emx ? sc : emx;
+        if (gs > ebest) {
+          ebest = gs;
+          epick = k;
+          es_k = sc;
+        }
+      }
+    }
+  }
+  for (int t0 = 0; !kHelp && t0 < cap; t0 += 16) {  // score of exec action k / N, k < cap, from [x_dag[:3], h_dag, h_glob, k/N]
     const int k = t0 + rl;
     const bool ok = k < cap;
     const float* xq = dp_opq(x);
@@ -680,6 +965,7 @@ __device__ __forceinline__ bool decima_policy_env(const Params* __restrict__ P, 
       }
     }
   }
+  lapf(8);  // (fine: exec tiles)
   emx = W::max_f(emx);
   scratch_sync<W, kGlobal>();
   float ez = 0.0f;

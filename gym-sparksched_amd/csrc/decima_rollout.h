@@ -67,17 +67,20 @@ struct DecimaRolloutArgs {
   // the wave's LDS, at byte plan_off of its scratch block (what the layout would give the row map and the rest of the
   // CU's share; the engine keeps its row map in the cold block). Larger ones use the env's global workspace.
   int32_t plan_cap, plan_off;
+  int32_t help_off;  // the exec-score helpers' mailbox (decima_policy.h DpHelp): byte offset in the workgroup's LDS
   ssim_decima_samples smp;  // smp.rec == nullptr: no sample arena
 };
 
 // The Decima decision of one env's current observation: its features (decima.h) and the fused policy
 // (decima_policy.h), with the features' scratch and the policy's plan in the wave's LDS at byte `plan_lds` when the
 // observation has at most `plan_cap` nodes (0: in the env's global workspace: feat_scratch / plan). (Inlined: as a
-// call, the calling convention saved every live register around it, 1.2 KB per lane of scratch.)
+// call, the calling convention saved every live register around it, 1.2 KB per lane of scratch.) kHelp: the exec
+// scores on the workgroup's helper waves, through the mailbox at LDS byte `help_lds` (decima_policy.h dp_exec_tiles).
+template <bool kHelp = false>
 __device__ __forceinline__ DpAction decima_decide(
     const Params* P0, const uint8_t* obs0, const dp_f32x4* weights0, uint8_t* feat_scratch0, uint8_t* plan0,
     float* feats0, int32_t* ccap0, uint32_t* emask0, int32_t* depth0, float num_tasks_scale, float work_scale,
-    uint64_t seed, uint64_t ctr, int eid, int plan_cap, uint32_t plan_lds, uint64_t* pprof) {
+    uint64_t seed, uint64_t ctr, int eid, int plan_cap, uint32_t plan_lds, uint64_t* pprof, uint32_t help_lds = 0) {
   using W = WaveHip;
   const Params* P = (const Params*)(const SSIM_GLOBAL Params*)P0;
   const uint8_t* obs = (const uint8_t*)(const SSIM_GLOBAL uint8_t*)obs0;
@@ -90,6 +93,7 @@ __device__ __forceinline__ DpAction decima_decide(
   const DecimaPolicyOut none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   const DpWGlobal wts{weights};
   DpAction act;
+  DpHelp* const help = kHelp ? reinterpret_cast<DpHelp*>(g_smem + help_lds) : nullptr;
 #ifdef SSIM_PROFILE
   uint64_t tp = W::clock();
 #endif
@@ -104,8 +108,8 @@ __device__ __forceinline__ DpAction decima_decide(
 #ifdef SSIM_PROFILE
     if (pprof != nullptr && W::lane() == 0) W::lds_add_u64(pprof - kPhDecParts + kPhDecFeat, W::clock() - tp);
 #endif
-    decima_policy_env<false>(P, obs, feats, ccap, emask, depth, wts, plan_cap, seed, ctr, eid, pl, none, &act, pprof,
-                             kDpLdsDags);
+    decima_policy_env<false, kHelp>(P, obs, feats, ccap, emask, depth, wts, plan_cap, seed, ctr, eid, pl, none, &act,
+                                    pprof, kDpLdsDags, help);
   } else {  // the env's global workspace
     uint8_t* fs = (uint8_t*)(SSIM_GLOBAL uint8_t*)feat_scratch0;
     uint8_t* pg = (uint8_t*)(SSIM_GLOBAL uint8_t*)plan0;
@@ -113,12 +117,13 @@ __device__ __forceinline__ DpAction decima_decide(
 #ifdef SSIM_PROFILE
     if (pprof != nullptr && W::lane() == 0) W::lds_add_u64(pprof - kPhDecParts + kPhDecFeat, W::clock() - tp);
 #endif
-    decima_policy_env<true>(P, obs, feats, ccap, emask, depth, wts, L.stage_cap, seed, ctr, eid, pg, none, &act,
-                            pprof);
+    decima_policy_env<true, kHelp>(P, obs, feats, ccap, emask, depth, wts, L.stage_cap, seed, ctr, eid, pg, none, &act,
+                                   pprof, 0, help);
   }
   return act;
 }
 
+template <bool kHelp = false>
 struct DecimaPolicy {
   const Params* P;
   const uint8_t* obs;
@@ -187,10 +192,10 @@ struct DecimaPolicy {
 #endif
     const bool lds_plan = n <= a.plan_cap && nj <= kDpLdsDags;
     SSIM_MARK("decima_policy_begin");
-    const DpAction act = decima_decide(P, obs, a.weights, wk + a.wl.feat_scratch, wk + a.wl.plan, feats, ccap, emask,
+    const DpAction act = decima_decide<kHelp>(P, obs, a.weights, wk + a.wl.feat_scratch, wk + a.wl.plan, feats, ccap, emask,
                                        depth, a.num_tasks_scale, a.work_scale, a.seed, ctr, eid,
                                        lds_plan ? a.plan_cap : 0,
-                                       (uint32_t)(s.scr + a.plan_off - g_smem), pprof);
+                                       (uint32_t)(s.scr + a.plan_off - g_smem), pprof, (uint32_t)a.help_off);
     SSIM_MARK("decima_policy_end");
 #ifdef SSIM_PROFILE
     s.prof_add(kPhDecPolicy, W::clock() - tp);
@@ -295,31 +300,49 @@ struct DecimaPolicy {
 #ifndef SSIM_DECIMA_ROLLOUT_WAVES
 #define SSIM_DECIMA_ROLLOUT_WAVES 4
 #endif
-// kN / kJ: executor count and job cap as compile-time constants (0 = read from the layout), as kernels.h.
-template <bool kRes, int kN, int kJ>
+// kN / kJ: executor count and job cap as compile-time constants (0 = read from the layout), as kernels.h. kHelp: the
+// workgroup is kDpHelpWaves waves; wave 0 runs the env, the others its exec-score tiles (decima_policy.h), until wave 0
+// publishes kDpHelpExit at the end of its rollout (every path out of rollout_body comes back here).
+template <bool kRes, int kN, int kJ, bool kHelp>
 __device__ __forceinline__ void decima_rollout_body(const Params* __restrict__ P, uint8_t* state, uint8_t* obs,
                                                     DecimaRolloutArgs a, int num_steps, int flags,
                                                     const double* __restrict__ limits, uint8_t* reset,
                                                     int32_t* action_log, int64_t budget, uint64_t* prof_out) {
+  DpHelp* const help = reinterpret_cast<DpHelp*>(g_smem + a.help_off);
+  if constexpr (kHelp) {
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (wv != 0) {
+      const DpWGlobal wts{(const dp_f32x4*)(const SSIM_GLOBAL dp_f32x4*)a.weights};
+      dp_help_loop(wts, help, kN > 0 ? kN : P->L.num_executors, wv);
+      return;
+    }
+  }
   a.autoreset = (flags & SSIM_ROLLOUT_AUTORESET) != 0;
   a.test_reject = (flags & SSIM_ROLLOUT_TEST_REJECT) != 0;
-  const DecimaPolicy pol{P, obs, a};
-  rollout_body<kRes, kN, kJ, 0, DecimaPolicy>(P, state, obs, pol, num_steps, flags, limits, reset, action_log, prof_out,
-                                              budget, nullptr, !kRes, SSIM_DR_EX_LDS != 0);
+  const DecimaPolicy<kHelp> pol{P, obs, a};
+  rollout_body<kRes, kN, kJ, 0, DecimaPolicy<kHelp>>(P, state, obs, pol, num_steps, flags, limits, reset, action_log,
+                                                     prof_out, budget, nullptr, !kRes, SSIM_DR_EX_LDS != 0);
+  if constexpr (kHelp) {
+    if (WaveHip::lane() == 0) help->cmd = kDpHelpExit;
+    __syncthreads();  // the helpers' barrier A: they read the exit and end
+  }
 }
 #define SSIM_DR_WAVES(kRes) ((kRes) ? 1 : SSIM_DECIMA_ROLLOUT_WAVES)
-template <bool kRes, int kN = 0, int kJ = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_DR_WAVES(kRes)))) void k_decima_rollout(
+#define SSIM_DR_THREADS(kHelp) ((kHelp) ? 64 * kDpHelpWaves : 64)
+template <bool kRes, int kN = 0, int kJ = 0, bool kHelp = false>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, SSIM_DR_THREADS(kHelp)), amdgpu_waves_per_eu(SSIM_DR_WAVES(kRes)))) void k_decima_rollout(
     const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
     const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget, uint64_t* prof_out) {
-  decima_rollout_body<kRes, kN, kJ>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
+  decima_rollout_body<kRes, kN, kJ, kHelp>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget,
+                                           prof_out);
 }
 // launches that are not measured (SSIM_ROLLOUT_WARMUP), under their own symbol
-template <bool kRes, int kN = 0, int kJ = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSIM_DR_WAVES(kRes)))) void k_decima_rollout_warmup(
+template <bool kRes, int kN = 0, int kJ = 0, bool kHelp = false>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, SSIM_DR_THREADS(kHelp)), amdgpu_waves_per_eu(SSIM_DR_WAVES(kRes)))) void k_decima_rollout_warmup(
     const Params* __restrict__ P, uint8_t* state, uint8_t* obs, DecimaRolloutArgs a, int num_steps, int flags,
     const double* __restrict__ limits, uint8_t* reset, int32_t* action_log, int64_t budget, uint64_t* prof_out) {
-  decima_rollout_body<kRes, kN, kJ>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget, prof_out);
+  decima_rollout_body<kRes, kN, kJ, kHelp>(P, state, obs, a, num_steps, flags, limits, reset, action_log, budget,
+                                           prof_out);
 }
 
 using DecimaRolloutFn = void (*)(const Params*, uint8_t*, uint8_t*, DecimaRolloutArgs, int, int, const double*,
@@ -328,6 +351,7 @@ struct DecimaRolloutSet {
   DecimaRolloutFn rollout, rollout_warmup;
   SetTraceFn set_trace;  // the set KAT through this unit's engine instantiation (kernels.h k_set_trace)
   const char* name;      // the translation unit (ssim_debug_kernel_name)
+  int waves = 1;         // waves per env's workgroup (kDpHelpWaves: the exec-score helpers)
 };
 DecimaRolloutSet decima_rollout_hbm();    // k_dr_hbm.hip
 DecimaRolloutSet decima_rollout_hbm50();  // k_dr_hbm50.hip: 50 executors / 200 jobs

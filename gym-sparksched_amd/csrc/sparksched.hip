@@ -587,12 +587,14 @@ extern "C" int ssim_decima_policy(ssim_handle* h, const float* node_feats, const
 // lowers the workgroups per CU the layout counted on).
 struct DecimaLdsPlan {
   int32_t cap, off;
-  int64_t lds;  // dynamic LDS of the launch
+  int64_t lds;       // dynamic LDS of the launch
+  int32_t help_off;  // the exec-score helpers' mailbox (units with helper waves), after the rest
 };
-static DecimaLdsPlan decima_lds_plan(const Params& P) {
+static DecimaLdsPlan decima_lds_plan(const Params& P, const DecimaRolloutSet& ks) {
   const StateOffsets& O = P.O;
   const ssim_layout& L = P.L;
-  DecimaLdsPlan pl{0, 0, O.lds_bytes};
+  DecimaLdsPlan pl{0, 0, O.lds_bytes, 0};
+  const int64_t help = ks.waves > 1 ? dp_help_bytes(L.num_executors) : 0;
   const int64_t eng = O.lds_resident ? O.hot_bytes + O.scratch_bytes : O.scratch_hbm_bytes;  // (HBM: row map cold)
   // Engines without the duration-descriptor cache hold only per-operation temporaries in their LDS scratch (set
   // tables, key lists, the commitment plan, observe()'s stage -> row map), none live across a decision: the plan
@@ -608,7 +610,7 @@ static DecimaLdsPlan decima_lds_plan(const Params& P) {
   const int64_t off = overlay ? (!O.lds_resident && SSIM_DR_EX_LDS ? O.sc_keys_a : 0)
                               : align16(O.lds_resident ? O.scratch_bytes : O.scratch_hbm_bytes);
   const int64_t base = O.lds_resident ? O.hot_bytes : 0;  // (the plan offset is relative to the scratch block)
-  const int64_t room = O.lds_share - base - off;
+  const int64_t room = O.lds_share - base - off - help;
   int cap = 0;
   while (cap < L.stage_cap && decima_policy_lds_bytes(cap + 1, kDpLdsDags) <= room &&
          decima_scratch_bytes(cap + 1) <= room)
@@ -619,12 +621,16 @@ static DecimaLdsPlan decima_lds_plan(const Params& P) {
     const int64_t need = base + off + decima_policy_lds_bytes(cap, kDpLdsDags);
     pl.lds = need > align16(eng) ? need : align16(eng);
   }
+  if (help > 0) {
+    pl.help_off = (int32_t)align16(pl.lds);
+    pl.lds = pl.help_off + help;
+  }
   return pl;
 }
 
 extern "C" int64_t ssim_decima_rollout_lds_bytes(const ssim_handle* h) {
   if (h == nullptr) return set_err(SSIM_E_ARG, "ssim_decima_rollout_lds_bytes: null handle");
-  return decima_lds_plan(h->params).lds;
+  return decima_lds_plan(h->params, pick_decima(h->params)).lds;
 }
 
 extern "C" int64_t ssim_decima_workspace_bytes(const ssim_handle* h) {
@@ -679,14 +685,15 @@ extern "C" int ssim_decima_rollout(ssim_handle* h, const float* params, int32_t 
   }
   const DecimaRolloutSet ks = pick_decima(h->params);
   const DecimaRolloutFn fn = (flags & SSIM_ROLLOUT_WARMUP) ? ks.rollout_warmup : ks.rollout;
-  const DecimaLdsPlan pl = decima_lds_plan(h->params);
+  const DecimaLdsPlan pl = decima_lds_plan(h->params, ks);
   a.plan_cap = pl.cap;
   a.plan_off = pl.off;
+  a.help_off = pl.help_off;
   const int64_t lds = pl.lds;
   const int rc = lds_opt_in((const void*)fn, lds);
   if (rc != SSIM_OK) return rc;
   if (total_decisions > 0 && h->ticket_slot) flags |= kFlagTicketSlot;
-  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64), (size_t)lds, (hipStream_t)stream, dparams(h),
+  hipLaunchKernelGGL(fn, dim3(L.num_envs), dim3(64 * ks.waves), (size_t)lds, (hipStream_t)stream, dparams(h),
                      h->state, h->obs, a, max_steps, flags, time_limits, h->reset, action_log, total_decisions,
                      h->prof_next);
   h->prof_next = nullptr;

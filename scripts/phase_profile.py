@@ -31,6 +31,8 @@ NUM_SLOTS = 40 + NSTAMPS + len(DEC_PHASES) + len(DEC_PARTS) + len(RESET_SLOTS)  
 
 def build_prof():
     out = os.path.join(REPO, "gym-sparksched_amd", "build", "libsparksched_prof.so")
+    if os.environ.get("SSIM_PROF_LIB"):  # another prebuilt diagnostic variant (e.g. -DSSIM_PROFILE_FINE)
+        return os.environ["SSIM_PROF_LIB"]
     if os.path.exists(out) and "--build" not in sys.argv:
         return out  # prebuilt in-tree (build on the CPU container: `python scripts/phase_profile.py --build`)
     import __graft_entry__
